@@ -1,0 +1,135 @@
+#!/usr/bin/env python3
+"""Headline benchmark: training tokens/s at seq-len 2048, data parallel over N MI355X.
+
+Config (BASELINE.json / BASELINE.md): Llama-3-8B-shaped decoder (reference
+train.py:43-53; vocab 131072 like the reference's Mistral-Nemo tokenizer),
+seq 2048, batch 1 per GPU, bf16 params/grads/AdamW states, lr 5e-5 with 100
+warmup steps, grad clipping at 1.0 — the reference's logged run (train.sh:16-20).
+Synthetic tokens, random-init weights (no network on the GPU box). Every timed
+step is a full training step: H2D of the batch, forward, backward with the
+bucketed RCCL all-reduce, gradient norm + clip, AdamW, LR-scheduler step.
+
+    python bench.py --gpus N --steps K --warmup W
+    torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU)
+
+Rank 0 prints one JSON line; ``value`` is the whole-job tokens/s (sum over
+GPUs), timed between barriers + device syncs, max step time over ranks.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+BASELINE_TOK_S_PER_GPU = 6376.0  # 1x GH200, Llama-3-8B, seq 2048, bs 1
+METRIC = "tokens/sec/GPU seq-len 2048 DP at 1/2/4/8 MI355X; checkpoint save wall-clock (s)"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--model", default="llama3-8b")
+    ap.add_argument("--seq-len", type=int, default=2048)
+    ap.add_argument("--batch-size", type=int, default=1)
+    ap.add_argument("--vocab-size", type=int, default=131072)
+    ap.add_argument("--bucket-mb", type=float, default=256.0)
+    ap.add_argument("--ckpt-dir", default="", help="also time one async checkpoint save into this dir")
+    ap.add_argument("--device", default="cuda")
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    from fault_tolerant_llm_training_amd.parallel import dist as fdist
+    from fault_tolerant_llm_training_amd.parallel.ddp import FlatDDP
+    from fault_tolerant_llm_training_amd.models.llama import build_model, model_args_for, flops_per_token
+    from fault_tolerant_llm_training_amd.optim.adamw import FlatAdamW
+    from fault_tolerant_llm_training_amd.utils.lr import build_lr_scheduler
+    from fault_tolerant_llm_training_amd.data.synthetic import SyntheticTokens
+
+    info = fdist.init_distributed(a.device)
+    dev = info.device
+    world = info.world_size
+    if a.gpus != world and info.is_main:
+        print(f"[bench] note: --gpus {a.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+
+    margs = model_args_for(a.model, vocab_size=a.vocab_size, seq_len=a.seq_len)
+    model = build_model(margs, dev, torch.bfloat16, seed=1234)
+    opt = FlatAdamW(model.parameters(), model.flat, lr=5e-5, max_grad_norm=1.0)
+    sched = build_lr_scheduler(opt, 100)
+    ddp = FlatDDP(model.flat, model.sinks_in_backward_order(), bucket_mb=a.bucket_mb)
+    ddp.broadcast_params()
+
+    data = SyntheticTokens(a.vocab_size, a.seq_len, seed=4321, rank=info.rank, world_size=world)
+    B, S = a.batch_size, a.seq_len
+    inv_count = torch.full((1,), 1.0 / (B * S * world), dtype=torch.float32, device=dev)
+
+    def step(i):
+        tok, lab = data.batch(i, B)
+        tok = tok.to(dev, non_blocking=True)
+        lab = lab.to(dev, non_blocking=True)
+        loss = model(tok, lab, inv_count)
+        loss.backward()
+        ddp.finish()
+        opt.clip_grad_norm_(1.0)
+        opt.step()
+        sched.step()
+        return loss
+
+    for i in range(a.warmup):
+        loss = step(i)
+    torch.cuda.synchronize()
+    fdist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        loss = step(a.warmup + i)
+    torch.cuda.synchronize()
+    fdist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    elapsed = fdist.ctrl_allreduce_max(int(elapsed * 1e9)) / 1e9
+    final_loss = float(loss.item())
+    opt.check_finite(block=True)
+
+    ms = elapsed / a.steps * 1e3
+    tok_s = B * S * world * a.steps / elapsed
+    fpt = flops_per_token(margs, S)
+    mfu = tok_s / world * fpt / 2.5e15
+    out = {
+        "metric": METRIC,
+        "value": round(tok_s, 1),
+        "unit": "tokens/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(ms, 2),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": round(tok_s / BASELINE_TOK_S_PER_GPU, 3),
+        "dtype": "bf16",
+        "data": "synthetic",
+        "config": {"model": a.model, "global_batch": B * world, "seq_len": S, "parallelism": f"dp{world}"},
+        "tokens_per_s_per_gpu": round(tok_s / world, 1),
+        "vs_baseline_per_gpu": round(tok_s / world / BASELINE_TOK_S_PER_GPU, 3),
+        "mfu_vs_2.5PF_dense": round(mfu, 4),
+        "final_loss": round(final_loss, 4),
+        "params": model.num_params(),
+    }
+    if a.ckpt_dir:
+        from fault_tolerant_llm_training_amd.ckpt.bench_save import time_checkpoint_save
+
+        out["ckpt_save"] = time_checkpoint_save(model, opt, sched, a.ckpt_dir, info)
+    if info.is_main:
+        print(json.dumps(out), flush=True)
+    fdist.destroy()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,307 @@
+// RMSNorm / LayerNorm (weight-only) forward + backward for gfx950.
+//
+// Math parity with the reference RMSNorm (reference model.py:24-48): the
+// normalisation runs in fp32, is rounded to the activation dtype, and only then
+// multiplied by the weight (`output = norm(x.float()).type_as(x) * weight`).
+// `norm_type="layernorm"` (reference model.py:19, declared but unused there)
+// selects the mean-subtracting variant.
+//
+// Layout: one wave (64 lanes) per row, 8 contiguous bf16 (one 16-B load) per
+// lane per 512-column chunk; the whole row stays in VGPRs between the reduction
+// and the write (one HBM read + one write per element). Backward writes
+// per-wave fp32 dW partials (no atomics → deterministic) that a column-parallel
+// kernel folds into the bf16 weight gradient, which is written straight into
+// the flat gradient buffer.
+#include "torch_utils.h"
+
+namespace {
+
+constexpr int ROWS_PER_BLOCK = 4;  // 4 waves x 64 lanes
+
+template <int CH, bool LN>
+__global__ __launch_bounds__(256) void norm_fwd_kernel(const bf16_t* __restrict__ x,
+                                                       const bf16_t* __restrict__ w,
+                                                       bf16_t* __restrict__ y,
+                                                       float* __restrict__ rstd,
+                                                       float* __restrict__ mean_out, int M,
+                                                       int N, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * ROWS_PER_BLOCK + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const bf16_t* xr = x + (size_t)row * N;
+  float v[CH][8];
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    const int idx = c * 512 + lane * 8;
+    if (idx < N) {
+      uint4 raw = *reinterpret_cast<const uint4*>(xr + idx);
+      unpack8(raw, v[c]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[c][j] = 0.f;
+    }
+    if (LN) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += v[c][j];
+    }
+  }
+  float mu = 0.f;
+  if (LN) mu = wave_sum(s) / (float)N;
+  float ss = 0.f;
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    const int idx = c * 512 + lane * 8;
+    if (idx < N) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float d = v[c][j] - mu;
+        ss += d * d;
+      }
+    }
+  }
+  ss = wave_sum(ss);
+  const float r = rsqrtf(ss / (float)N + eps);
+  bf16_t* yr = y + (size_t)row * N;
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    const int idx = c * 512 + lane * 8;
+    if (idx < N) {
+      float wf[8], o[8];
+      unpack8(*reinterpret_cast<const uint4*>(w + idx), wf);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = bf2f(f2bf((v[c][j] - mu) * r)) * wf[j];
+      *reinterpret_cast<uint4*>(yr + idx) = pack8(o);
+    }
+  }
+  if (lane == 0) {
+    rstd[row] = r;
+    if (LN) mean_out[row] = mu;
+  }
+}
+
+// dx = r * (dn - mean(dn) [LN only] - n * mean(dn * n)),  dn = dy * w, n = (x - mu) * r
+// dw_partial[wave_slot][col] += dy * n
+template <int CH, bool LN>
+__global__ __launch_bounds__(256) void norm_bwd_kernel(
+    const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
+    const float* __restrict__ rstd, const float* __restrict__ mean_in, bf16_t* __restrict__ dx,
+    const bf16_t* __restrict__ dres, float* __restrict__ dw_part, int M, int N) {
+  // Row data is kept packed (bf16) in VGPRs; fp32 values are recomputed per pass
+  // to keep the register footprint at ~3 x CH x 4 + 8 x CH VGPRs.
+  const int lane = threadIdx.x & 63;
+  const int slot = blockIdx.x * ROWS_PER_BLOCK + (threadIdx.x >> 6);
+  const int nslots = gridDim.x * ROWS_PER_BLOCK;
+  uint4 wr[CH];
+  float acc[CH][8];
+  const uint4 z = make_uint4(0, 0, 0, 0);
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    const int idx = c * 512 + lane * 8;
+    wr[c] = idx < N ? *reinterpret_cast<const uint4*>(w + idx) : z;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[c][j] = 0.f;
+  }
+  const float invN = 1.f / (float)N;
+  for (int row = slot; row < M; row += nslots) {
+    const float r = rstd[row];
+    const float mu = LN ? mean_in[row] : 0.f;
+    const bf16_t* xr = x + (size_t)row * N;
+    const bf16_t* dyr = dy + (size_t)row * N;
+    uint4 xv[CH], gv[CH];
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const int idx = c * 512 + lane * 8;
+      xv[c] = idx < N ? *reinterpret_cast<const uint4*>(xr + idx) : z;
+      gv[c] = idx < N ? *reinterpret_cast<const uint4*>(dyr + idx) : z;
+    }
+    float sdn = 0.f, sdnn = 0.f;
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      float xf[8], g[8], wf[8];
+      unpack8(xv[c], xf);
+      unpack8(gv[c], g);
+      unpack8(wr[c], wf);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float n = (xf[j] - mu) * r;
+        const float dn = g[j] * wf[j];
+        acc[c][j] += g[j] * n;
+        sdn += dn;
+        sdnn += dn * n;
+      }
+    }
+    sdnn = wave_sum(sdnn) * invN;
+    if (LN) sdn = wave_sum(sdn) * invN;
+    bf16_t* dxr = dx + (size_t)row * N;
+    const bf16_t* drr = dres ? dres + (size_t)row * N : nullptr;
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const int idx = c * 512 + lane * 8;
+      if (idx < N) {
+        float xf[8], g[8], wf[8], o[8];
+        unpack8(xv[c], xf);
+        unpack8(gv[c], g);
+        unpack8(wr[c], wf);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float n = (xf[j] - mu) * r;
+          o[j] = r * (g[j] * wf[j] - (LN ? sdn : 0.f) - n * sdnn);
+        }
+        if (drr) {
+          float rr[8];
+          unpack8(*reinterpret_cast<const uint4*>(drr + idx), rr);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] += rr[j];
+        }
+        *reinterpret_cast<uint4*>(dxr + idx) = pack8(o);
+      }
+    }
+  }
+  float* part = dw_part + (size_t)slot * N;
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    const int idx = c * 512 + lane * 8;
+    if (idx < N) {
+      *reinterpret_cast<float4*>(part + idx) = make_float4(acc[c][0], acc[c][1], acc[c][2], acc[c][3]);
+      *reinterpret_cast<float4*>(part + idx + 4) = make_float4(acc[c][4], acc[c][5], acc[c][6], acc[c][7]);
+    }
+  }
+}
+
+// Column sums of a [P, N] fp32 slab -> bf16 dw (optionally accumulated).
+// Block = 64 columns x 4 row groups; fixed summation order (deterministic).
+__global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ part,
+                                                     bf16_t* __restrict__ dw, int P, int N,
+                                                     bool accumulate) {
+  __shared__ float red[4][64];
+  const int col = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int g = threadIdx.x >> 6;
+  float s = 0.f;
+  if (col < N) {
+    for (int p = g; p < P; p += 4) s += part[(size_t)p * N + col];
+  }
+  red[g][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (g == 0 && col < N) {
+    float t = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+    if (accumulate) t += bf2f(dw[col]);
+    dw[col] = f2bf(t);
+  }
+}
+
+template <bool LN>
+void launch_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, float* rstd, float* mean, int M,
+                int N, float eps, hipStream_t st) {
+  const int chunks = (N + 511) / 512;
+  dim3 grid((M + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK), block(256);
+#define FT_NF(C)                                                                              \
+  hipLaunchKernelGGL((norm_fwd_kernel<C, LN>), grid, block, 0, st, x, w, y, rstd, mean, M, N, \
+                     eps)
+  if (chunks <= 1) FT_NF(1);
+  else if (chunks <= 2) FT_NF(2);
+  else if (chunks <= 4) FT_NF(4);
+  else if (chunks <= 8) FT_NF(8);
+  else if (chunks <= 16) FT_NF(16);
+  else TORCH_CHECK(false, "norm: N too large");
+#undef FT_NF
+}
+
+template <bool LN>
+void launch_bwd(const bf16_t* dy, const bf16_t* x, const bf16_t* w, const float* rstd,
+                const float* mean, bf16_t* dx, const bf16_t* dres, float* part, int nblk, int M,
+                int N, hipStream_t st) {
+  const int chunks = (N + 511) / 512;
+  dim3 grid(nblk), block(256);
+#define FT_NB(C)                                                                          \
+  hipLaunchKernelGGL((norm_bwd_kernel<C, LN>), grid, block, 0, st, dy, x, w, rstd, mean, dx, \
+                     dres, part, M, N)
+  if (chunks <= 1) FT_NB(1);
+  else if (chunks <= 2) FT_NB(2);
+  else if (chunks <= 4) FT_NB(4);
+  else if (chunks <= 8) FT_NB(8);
+  else if (chunks <= 16) FT_NB(16);
+  else TORCH_CHECK(false, "norm: N too large");
+#undef FT_NB
+}
+
+}  // namespace
+
+// Returns (y, rstd, mean). `mean` is empty for RMSNorm.
+std::tuple<at::Tensor, at::Tensor, at::Tensor> norm_fwd(const at::Tensor& x, const at::Tensor& w,
+                                                       double eps, bool layernorm) {
+  FT_CHECK_CUDA(x);
+  FT_CHECK_BF16(x);
+  FT_CHECK_BF16(w);
+  FT_CHECK_CONTIG(x);
+  FT_CHECK_CONTIG(w);
+  const int N = x.size(-1);
+  TORCH_CHECK(w.numel() == N, "norm: weight size mismatch");
+  TORCH_CHECK(N % 8 == 0, "norm: N must be a multiple of 8");
+  const int M = x.numel() / N;
+  const at::DeviceGuard guard(x.device());
+  auto y = at::empty_like(x);
+  auto rstd = at::empty({M}, x.options().dtype(at::kFloat));
+  at::Tensor mean = at::empty({layernorm ? M : 0}, x.options().dtype(at::kFloat));
+  if (M == 0) return {y, rstd, mean};
+  if (layernorm)
+    launch_fwd<true>(cptr<bf16_t>(x), cptr<bf16_t>(w), mptr<bf16_t>(y), mptr<float>(rstd),
+                     mptr<float>(mean), M, N, (float)eps, ft_stream());
+  else
+    launch_fwd<false>(cptr<bf16_t>(x), cptr<bf16_t>(w), mptr<bf16_t>(y), mptr<float>(rstd),
+                      nullptr, M, N, (float)eps, ft_stream());
+  FT_LAUNCH_CHECK();
+  return {y, rstd, mean};
+}
+
+// Returns dx; writes (or accumulates) dw into `dw` (a view into the flat grad buffer).
+// `dres` (optional) is added into dx: the residual-stream gradient fused into the norm.
+at::Tensor norm_bwd(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& w,
+                    const at::Tensor& rstd, const std::optional<at::Tensor>& mean,
+                    const at::Tensor& dw, const std::optional<at::Tensor>& dres,
+                    bool accumulate) {
+  FT_CHECK_CUDA(dy);
+  FT_CHECK_BF16(dy);
+  FT_CHECK_CONTIG(dy);
+  FT_CHECK_CONTIG(x);
+  FT_CHECK_BF16(dw);
+  FT_CHECK_CONTIG(dw);
+  const int N = x.size(-1);
+  const int M = x.numel() / N;
+  TORCH_CHECK(dy.numel() == x.numel() && dw.numel() == N, "norm_bwd: shape mismatch");
+  const at::DeviceGuard guard(x.device());
+  auto dx = at::empty_like(x);
+  const bool ln = mean.has_value() && mean->defined() && mean->numel() > 0;
+  const bf16_t* dr = nullptr;
+  if (dres.has_value() && dres->defined()) {
+    FT_CHECK_CONTIG((*dres));
+    TORCH_CHECK(dres->numel() == x.numel(), "norm_bwd: dres shape mismatch");
+    dr = cptr<bf16_t>(*dres);
+  }
+  int nblk = std::max(1, std::min((M + ROWS_PER_BLOCK * 8 - 1) / (ROWS_PER_BLOCK * 8), 64));
+  auto part = at::empty({(long)nblk * ROWS_PER_BLOCK, N}, x.options().dtype(at::kFloat));
+  if (M > 0) {
+    if (ln)
+      launch_bwd<true>(cptr<bf16_t>(dy), cptr<bf16_t>(x), cptr<bf16_t>(w), cptr<float>(rstd),
+                       cptr<float>(*mean), mptr<bf16_t>(dx), dr, mptr<float>(part), nblk, M, N,
+                       ft_stream());
+    else
+      launch_bwd<false>(cptr<bf16_t>(dy), cptr<bf16_t>(x), cptr<bf16_t>(w), cptr<float>(rstd),
+                        nullptr, mptr<bf16_t>(dx), dr, mptr<float>(part), nblk, M, N,
+                        ft_stream());
+    FT_LAUNCH_CHECK();
+  }
+  hipLaunchKernelGGL(colsum_kernel, dim3((N + 63) / 64), dim3(256), 0, ft_stream(),
+                     cptr<float>(part), mptr<bf16_t>(dw), nblk * ROWS_PER_BLOCK, N, accumulate);
+  FT_LAUNCH_CHECK();
+  return dx;
+}
+
+TORCH_LIBRARY_FRAGMENT(ftamd, m) {
+  m.def("norm_fwd(Tensor x, Tensor w, float eps, bool layernorm) -> (Tensor, Tensor, Tensor)",
+        &norm_fwd);
+  m.def(
+      "norm_bwd(Tensor dy, Tensor x, Tensor w, Tensor rstd, Tensor? mean, Tensor(a!) dw, "
+      "Tensor? dres, bool accumulate) -> Tensor",
+      &norm_bwd);
+}

@@ -1,0 +1,29 @@
+// Host-side glue between at::Tensor and the gfx950 kernels.
+#pragma once
+
+#include <ATen/ATen.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
+#include <c10/core/DeviceGuard.h>
+#include <torch/library.h>
+
+#include "common.h"
+
+static inline hipStream_t ft_stream() {
+  return at::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
+}
+
+#define FT_CHECK_CUDA(t) TORCH_CHECK((t).is_cuda(), #t " must be a GPU tensor")
+#define FT_CHECK_CONTIG(t) TORCH_CHECK((t).is_contiguous(), #t " must be contiguous")
+#define FT_CHECK_BF16(t) TORCH_CHECK((t).scalar_type() == at::kBFloat16, #t " must be bf16")
+#define FT_CHECK_F32(t) TORCH_CHECK((t).scalar_type() == at::kFloat, #t " must be fp32")
+
+#define FT_LAUNCH_CHECK() FT_HIP_CHECK(hipGetLastError())
+
+template <typename T>
+static inline const T* cptr(const at::Tensor& t) {
+  return reinterpret_cast<const T*>(t.data_ptr());
+}
+template <typename T>
+static inline T* mptr(const at::Tensor& t) {
+  return reinterpret_cast<T*>(t.data_ptr());
+}

@@ -1,0 +1,65 @@
+// pybind11 bindings for the native fault-tolerance runtime (`_runtime.so`).
+#include <hip/hip_runtime_api.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+#include <torch/extension.h>
+
+#include "runtime.h"
+
+namespace py = pybind11;
+using namespace ftrt;
+
+static torch::Tensor pinned_empty(uint64_t nbytes) {
+  uintptr_t p = pinned_alloc(nbytes);
+  return torch::from_blob(
+      reinterpret_cast<void*>(p), {(int64_t)nbytes},
+      [](void* q) { hipHostFree(q); },
+      torch::TensorOptions().dtype(torch::kUInt8).device(torch::kCPU));
+}
+
+PYBIND11_MODULE(_runtime, m) {
+  m.doc() = "Native fault-tolerance runtime: signal flags, snapshot engine, zip checkpoint writer";
+
+  m.def("signals_install", &signals_install);
+  m.def("signals_restore_default", &signals_restore_default);
+  m.def("signals_pending", &signals_pending);
+  m.def("signals_mask", &signals_mask);
+  m.def("signals_count", &signals_count);
+  m.def("signals_clear", &signals_clear);
+  m.def("signals_block", &signals_block, py::arg("signums"), py::arg("block"));
+
+  py::class_<ZipStats>(m, "ZipStats")
+      .def_readonly("seconds", &ZipStats::seconds)
+      .def_readonly("write_seconds", &ZipStats::write_seconds)
+      .def_readonly("fsync_seconds", &ZipStats::fsync_seconds)
+      .def_readonly("wait_seconds", &ZipStats::wait_seconds)
+      .def_readonly("bytes", &ZipStats::bytes)
+      .def_readonly("error", &ZipStats::error);
+
+  py::class_<ZipWriter>(m, "ZipWriter")
+      .def(py::init<std::string, std::string, std::string, int, uint64_t>(), py::arg("tmp_path"),
+           py::arg("final_path"), py::arg("archive"), py::arg("nthreads") = 8,
+           py::arg("chunk_bytes") = (64ull << 20))
+      .def("add_bytes",
+           [](ZipWriter& w, const std::string& name, py::bytes b) { w.add_bytes(name, std::string(b)); })
+      .def("add_buffer", &ZipWriter::add_buffer)
+      .def("total_size", &ZipWriter::total_size)
+      .def("start", &ZipWriter::start, py::arg("wait_event") = 0, py::arg("fsync") = true)
+      .def("run_sync", &ZipWriter::run_sync, py::arg("wait_event") = 0, py::arg("fsync") = true,
+           py::call_guard<py::gil_scoped_release>())
+      .def("done", &ZipWriter::done)
+      .def("wait", &ZipWriter::wait, py::call_guard<py::gil_scoped_release>());
+
+  py::class_<SnapshotEngine>(m, "SnapshotEngine")
+      .def(py::init<int>())
+      .def("begin", &SnapshotEngine::begin)
+      .def("copy", &SnapshotEngine::copy)
+      .def("mark", &SnapshotEngine::mark)
+      .def("stream_wait", &SnapshotEngine::stream_wait)
+      .def("query", &SnapshotEngine::query)
+      .def("sync", &SnapshotEngine::sync, py::call_guard<py::gil_scoped_release>())
+      .def("event_handle", &SnapshotEngine::event_handle)
+      .def("stream_handle", &SnapshotEngine::stream_handle);
+
+  m.def("pinned_empty", &pinned_empty, "Exact-size pinned host buffer (hipHostMalloc) as a uint8 tensor");
+}

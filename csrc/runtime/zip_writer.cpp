@@ -1,0 +1,330 @@
+// Native writer for PyTorch-format (zip) checkpoints.
+//
+// The reference writes its checkpoint with a synchronous torch.save straight to
+// the final path (reference utils.py:74-80; ~33.6 s for 48 GB, non-atomic —
+// SURVEY.md §A.6). This writer keeps the same on-disk format (a torch.load-able
+// zip: archive/data.pkl + archive/data/<key> storages, 64-B aligned, zip64) but
+// writes from host memory with a thread pool that checksums and pwrite()s
+// 64 MiB chunks in parallel, then publishes atomically (fsync + rename + dir
+// fsync). data.pkl is produced by torch's own pickler in Python.
+#include <errno.h>
+#include <fcntl.h>
+#include <string.h>
+#include <sys/stat.h>
+#include <unistd.h>
+#include <zlib.h>
+
+#include <chrono>
+#include <hip/hip_runtime_api.h>
+
+#include "runtime.h"
+
+namespace ftrt {
+namespace {
+
+constexpr uint64_t U32MAX = 0xFFFFFFFFull;
+constexpr uint64_t ALIGN = 64;
+constexpr uint16_t DOS_TIME = 0;
+constexpr uint16_t DOS_DATE = (0 << 9) | (1 << 5) | 1;  // 1980-01-01
+
+struct Buf {
+  std::string s;
+  void u16(uint16_t v) { s.append(reinterpret_cast<const char*>(&v), 2); }
+  void u32(uint32_t v) { s.append(reinterpret_cast<const char*>(&v), 4); }
+  void u64(uint64_t v) { s.append(reinterpret_cast<const char*>(&v), 8); }
+  void str(const std::string& v) { s.append(v); }
+};
+
+void pwrite_all(int fd, const void* p, uint64_t n, uint64_t off) {
+  const char* c = static_cast<const char*>(p);
+  while (n > 0) {
+    ssize_t w = ::pwrite(fd, c, n > (1ull << 30) ? (1ull << 30) : n, (off_t)off);
+    if (w < 0) {
+      if (errno == EINTR) continue;
+      throw std::runtime_error(std::string("pwrite failed: ") + strerror(errno));
+    }
+    c += w;
+    n -= (uint64_t)w;
+    off += (uint64_t)w;
+  }
+}
+
+double now() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
+std::string dirname_of(const std::string& p) {
+  auto pos = p.find_last_of('/');
+  if (pos == std::string::npos) return ".";
+  if (pos == 0) return "/";
+  return p.substr(0, pos);
+}
+
+}  // namespace
+
+ZipWriter::ZipWriter(std::string tmp_path, std::string final_path, std::string archive,
+                     int nthreads, uint64_t chunk_bytes)
+    : tmp_(std::move(tmp_path)),
+      final_(std::move(final_path)),
+      archive_(std::move(archive)),
+      nthreads_(nthreads < 1 ? 1 : nthreads),
+      chunk_(chunk_bytes ? chunk_bytes : (64ull << 20)) {}
+
+ZipWriter::~ZipWriter() {
+  if (th_.joinable()) th_.join();
+}
+
+void ZipWriter::add_bytes(const std::string& name, const std::string& bytes) {
+  ZipRecord r;
+  r.name = archive_ + "/" + name;
+  r.owned = bytes;
+  r.size = bytes.size();
+  recs_.push_back(std::move(r));
+  laid_out_ = false;
+}
+
+void ZipWriter::add_buffer(const std::string& name, uintptr_t ptr, uint64_t nbytes) {
+  ZipRecord r;
+  r.name = archive_ + "/" + name;
+  r.data = reinterpret_cast<const uint8_t*>(ptr);
+  r.size = nbytes;
+  recs_.push_back(std::move(r));
+  laid_out_ = false;
+}
+
+void ZipWriter::layout() {
+  uint64_t off = 0;
+  for (auto& r : recs_) {
+    if (!r.owned.empty() || r.data == nullptr) r.data = reinterpret_cast<const uint8_t*>(r.owned.data());
+    r.header_off = off;
+    const bool z64_local = r.size >= U32MAX;
+    r.zip64 = z64_local;
+    uint64_t base = off + 30 + r.name.size() + (z64_local ? 20 : 0) + 4;  // + FB header
+    uint64_t pad = (ALIGN - base % ALIGN) % ALIGN;
+    r.extra_len = (uint16_t)((z64_local ? 20 : 0) + 4 + pad);
+    r.data_off = base + pad;
+    off = r.data_off + r.size;
+  }
+  cd_off_ = off;
+  laid_out_ = true;
+}
+
+uint64_t ZipWriter::total_size() {
+  if (!laid_out_) layout();
+  return cd_off_;
+}
+
+void ZipWriter::start(uintptr_t wait_event, bool do_fsync) {
+  if (th_.joinable()) throw std::runtime_error("ZipWriter already started");
+  if (!laid_out_) layout();
+  th_ = std::thread([this, wait_event, do_fsync] { run(wait_event, do_fsync); });
+}
+
+void ZipWriter::run_sync(uintptr_t wait_event, bool do_fsync) {
+  if (!laid_out_) layout();
+  run(wait_event, do_fsync);
+}
+
+ZipStats ZipWriter::wait() {
+  if (th_.joinable()) th_.join();
+  return stats_;
+}
+
+void ZipWriter::run(uintptr_t wait_event, bool do_fsync) {
+  const double t0 = now();
+  int fd = -1;
+  try {
+    if (wait_event) {
+      hipError_t e = hipEventSynchronize(reinterpret_cast<hipEvent_t>(wait_event));
+      if (e != hipSuccess) throw std::runtime_error(std::string("hipEventSynchronize: ") + hipGetErrorString(e));
+    }
+    const double t1 = now();
+    stats_.wait_seconds = t1 - t0;
+    fd = ::open(tmp_.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
+    if (fd < 0) throw std::runtime_error("open(" + tmp_ + "): " + strerror(errno));
+
+    // ---- data records: parallel CRC + pwrite in chunks --------------------------
+    struct Chunk {
+      size_t rec;
+      uint64_t off, len;
+      uint32_t crc;
+    };
+    std::vector<Chunk> chunks;
+    for (size_t i = 0; i < recs_.size(); ++i) {
+      const auto& r = recs_[i];
+      if (r.size == 0) chunks.push_back({i, 0, 0, 0});
+      for (uint64_t o = 0; o < r.size; o += chunk_) chunks.push_back({i, o, std::min(chunk_, r.size - o), 0});
+    }
+    std::atomic<size_t> next{0};
+    std::string err;
+    std::mutex err_mu;
+    auto worker = [&] {
+      for (;;) {
+        size_t k = next.fetch_add(1);
+        if (k >= chunks.size()) return;
+        Chunk& c = chunks[k];
+        const auto& r = recs_[c.rec];
+        try {
+          const uint8_t* p = r.data + c.off;
+          uLong crc = crc32(0L, Z_NULL, 0);
+          uint64_t done = 0;
+          while (done < c.len) {
+            const uInt n = (uInt)std::min<uint64_t>(c.len - done, 1u << 30);
+            crc = crc32(crc, p + done, n);
+            done += n;
+          }
+          c.crc = (uint32_t)crc;
+          if (c.len) pwrite_all(fd, p, c.len, r.data_off + c.off);
+        } catch (const std::exception& ex) {
+          std::lock_guard<std::mutex> g(err_mu);
+          err = ex.what();
+          next.store(chunks.size());
+        }
+      }
+    };
+    std::vector<std::thread> pool;
+    const int nt = (int)std::min<size_t>(nthreads_, std::max<size_t>(1, chunks.size()));
+    for (int t = 0; t < nt; ++t) pool.emplace_back(worker);
+    for (auto& t : pool) t.join();
+    if (!err.empty()) throw std::runtime_error(err);
+    for (auto& r : recs_) r.crc = 0;
+    {
+      std::vector<bool> first(recs_.size(), true);
+      for (const auto& c : chunks) {
+        auto& r = recs_[c.rec];
+        if (first[c.rec]) {
+          r.crc = c.crc;
+          first[c.rec] = false;
+        } else {
+          r.crc = (uint32_t)crc32_combine64(r.crc, c.crc, (z_off64_t)c.len);
+        }
+      }
+    }
+
+    // ---- local headers ----------------------------------------------------------
+    for (const auto& r : recs_) {
+      Buf b;
+      b.u32(0x04034b50);
+      b.u16(r.zip64 ? 45 : 20);
+      b.u16(0);
+      b.u16(0);
+      b.u16(DOS_TIME);
+      b.u16(DOS_DATE);
+      b.u32(r.crc);
+      b.u32(r.zip64 ? (uint32_t)U32MAX : (uint32_t)r.size);
+      b.u32(r.zip64 ? (uint32_t)U32MAX : (uint32_t)r.size);
+      b.u16((uint16_t)r.name.size());
+      b.u16(r.extra_len);
+      b.str(r.name);
+      uint16_t used = 0;
+      if (r.zip64) {
+        b.u16(0x0001);
+        b.u16(16);
+        b.u64(r.size);
+        b.u64(r.size);
+        used = 20;
+      }
+      const uint16_t pad = (uint16_t)(r.extra_len - used - 4);
+      b.u16(0x4246);  // "FB": PyTorch's alignment padding field
+      b.u16(pad);
+      b.s.append(pad, 'Z');
+      pwrite_all(fd, b.s.data(), b.s.size(), r.header_off);
+    }
+
+    // ---- central directory --------------------------------------------------------
+    Buf cd;
+    bool need64 = recs_.size() >= 0xFFFF;
+    for (const auto& r : recs_) {
+      const bool big = r.size >= U32MAX;
+      const bool far = r.header_off >= U32MAX;
+      std::string ex;
+      Buf e;
+      if (big || far) {
+        e.u16(0x0001);
+        e.u16((uint16_t)((big ? 16 : 0) + (far ? 8 : 0)));
+        if (big) {
+          e.u64(r.size);
+          e.u64(r.size);
+        }
+        if (far) e.u64(r.header_off);
+        need64 = true;
+      }
+      cd.u32(0x02014b50);
+      cd.u16(45);
+      cd.u16((big || far) ? 45 : 20);
+      cd.u16(0);
+      cd.u16(0);
+      cd.u16(DOS_TIME);
+      cd.u16(DOS_DATE);
+      cd.u32(r.crc);
+      cd.u32(big ? (uint32_t)U32MAX : (uint32_t)r.size);
+      cd.u32(big ? (uint32_t)U32MAX : (uint32_t)r.size);
+      cd.u16((uint16_t)r.name.size());
+      cd.u16((uint16_t)e.s.size());
+      cd.u16(0);
+      cd.u16(0);
+      cd.u16(0);
+      cd.u32(0);
+      cd.u32(far ? (uint32_t)U32MAX : (uint32_t)r.header_off);
+      cd.str(r.name);
+      cd.str(e.s);
+    }
+    const uint64_t cd_size = cd.s.size();
+    if (cd_off_ >= U32MAX || cd_size >= U32MAX) need64 = true;
+    Buf tail;
+    const uint64_t n = recs_.size();
+    if (need64) {
+      const uint64_t z64_off = cd_off_ + cd_size;
+      tail.u32(0x06064b50);
+      tail.u64(44);
+      tail.u16(45);
+      tail.u16(45);
+      tail.u32(0);
+      tail.u32(0);
+      tail.u64(n);
+      tail.u64(n);
+      tail.u64(cd_size);
+      tail.u64(cd_off_);
+      tail.u32(0x07064b50);
+      tail.u32(0);
+      tail.u64(z64_off);
+      tail.u32(1);
+    }
+    tail.u32(0x06054b50);
+    tail.u16(0);
+    tail.u16(0);
+    tail.u16((uint16_t)std::min<uint64_t>(n, 0xFFFF));
+    tail.u16((uint16_t)std::min<uint64_t>(n, 0xFFFF));
+    tail.u32(cd_size >= U32MAX ? (uint32_t)U32MAX : (uint32_t)cd_size);
+    tail.u32(cd_off_ >= U32MAX ? (uint32_t)U32MAX : (uint32_t)cd_off_);
+    tail.u16(0);
+    cd.str(tail.s);
+    pwrite_all(fd, cd.s.data(), cd.s.size(), cd_off_);
+    stats_.bytes = cd_off_ + cd.s.size();
+    const double t2 = now();
+    stats_.write_seconds = t2 - t1;
+    if (do_fsync && ::fsync(fd) != 0) throw std::runtime_error(std::string("fsync: ") + strerror(errno));
+    ::close(fd);
+    fd = -1;
+    if (tmp_ != final_) {
+      if (::rename(tmp_.c_str(), final_.c_str()) != 0)
+        throw std::runtime_error("rename(" + tmp_ + "): " + strerror(errno));
+      if (do_fsync) {
+        int dfd = ::open(dirname_of(final_).c_str(), O_RDONLY | O_DIRECTORY | O_CLOEXEC);
+        if (dfd >= 0) {
+          ::fsync(dfd);
+          ::close(dfd);
+        }
+      }
+    }
+    stats_.fsync_seconds = now() - t2;
+  } catch (const std::exception& ex) {
+    stats_.error = ex.what();
+    if (fd >= 0) ::close(fd);
+  }
+  stats_.seconds = now() - t0;
+  done_.store(true);
+}
+
+}  // namespace ftrt

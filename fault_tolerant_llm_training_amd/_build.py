@@ -1,0 +1,170 @@
+"""In-tree build of the native components with explicit ``hipcc`` (gfx950 only).
+
+Two shared objects are produced next to this file:
+
+* ``_kernels.so`` — the hand-written CDNA4 HIP kernels (``csrc/kernels/*.hip``),
+  registered as ``torch.ops.ftamd.*`` through ``TORCH_LIBRARY_FRAGMENT``.
+* ``_runtime.so`` — the C++ runtime (``csrc/runtime/*.cpp``): async-signal-safe
+  signal flags, the pinned-host checkpoint snapshot engine and the checkpoint
+  writer thread, exposed through pybind11.
+
+No hipify, no ``torch.utils.cpp_extension`` JIT: sources are compiled directly
+with ``hipcc --offload-arch=gfx950`` and linked against the HIP runtime that
+ships inside the installed PyTorch wheel (both carry SONAME
+``libamdhip64.so.7``, so one runtime is loaded per process).
+
+Usage: ``python -m fault_tolerant_llm_training_amd._build [-j N] [--force]``.
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import os
+import subprocess
+import sys
+import sysconfig
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+ROOT = PKG.parent
+CSRC = ROOT / "csrc"
+BUILD = ROOT / "build"
+ARCH = os.environ.get("FT_OFFLOAD_ARCH", "gfx950")
+
+KERNELS_SO = PKG / "_kernels.so"
+RUNTIME_SO = PKG / "_runtime.so"
+
+
+def _torch_paths():
+    import torch
+
+    tdir = Path(torch.__file__).resolve().parent
+    return tdir / "include", tdir / "lib", int(torch._C._GLIBCXX_USE_CXX11_ABI)
+
+
+def _hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", "hipcc"):
+        if cand and (os.path.isabs(cand) and os.path.exists(cand) or not os.path.isabs(cand)):
+            return cand
+    return "hipcc"
+
+
+def _common_flags(ext_name: str):
+    inc, _lib, abi = _torch_paths()
+    import pybind11
+
+    return [
+        "-O3",
+        "-std=c++17",
+        "-fPIC",
+        f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
+        "-D__HIP_PLATFORM_AMD__=1",
+        "-DUSE_ROCM=1",
+        "-DHIPBLAS_V2",
+        "-D__HIP_NO_HALF_OPERATORS__=1",
+        "-D__HIP_NO_HALF_CONVERSIONS__=1",
+        "-DTORCH_API_INCLUDE_EXTENSION_H",
+        f"-DTORCH_EXTENSION_NAME={ext_name}",
+        "-I",
+        str(inc),
+        "-I",
+        str(inc / "torch" / "csrc" / "api" / "include"),
+        "-I",
+        sysconfig.get_paths()["include"],
+        "-I",
+        pybind11.get_include(),
+        "-I",
+        str(CSRC / "kernels"),
+        "-I",
+        str(CSRC / "runtime"),
+        "-Wno-unused-result",
+        "-Wno-ignored-attributes",
+        "-Wno-deprecated-declarations",
+    ]
+
+
+def _needs(obj: Path, src: Path, headers) -> bool:
+    if not obj.exists():
+        return True
+    t = obj.stat().st_mtime
+    if src.stat().st_mtime > t:
+        return True
+    return any(h.stat().st_mtime > t for h in headers)
+
+
+def _compile(src: Path, obj: Path, flags, device: bool):
+    cmd = [_hipcc()] + flags
+    if device:
+        cmd += [f"--offload-arch={ARCH}", "-x", "hip"]
+    cmd += ["-c", str(src), "-o", str(obj)]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"compile failed: {src}\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    return obj
+
+
+def _link(objs, out: Path, device: bool, extra=()):
+    _inc, lib, _ = _torch_paths()
+    cmd = [_hipcc(), "-shared", "-fPIC"]
+    if device:
+        cmd += [f"--offload-arch={ARCH}"]
+    cmd += [str(o) for o in objs]
+    cmd += [
+        "-L",
+        str(lib),
+        "-lc10",
+        "-lc10_hip",
+        "-ltorch",
+        "-ltorch_cpu",
+        "-ltorch_hip",
+        "-lamdhip64",
+        f"-Wl,-rpath,{lib}",
+        *extra,
+        "-o",
+        str(out) + ".tmp",
+    ]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"link failed: {out}\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    os.replace(str(out) + ".tmp", out)
+
+
+def build(jobs: int = 0, force: bool = False, verbose: bool = True) -> None:
+    BUILD.mkdir(exist_ok=True)
+    jobs = jobs or min(8, os.cpu_count() or 4)
+    targets = [
+        (KERNELS_SO, sorted((CSRC / "kernels").glob("*.hip")), CSRC / "kernels", "_kernels", True, ()),
+        (RUNTIME_SO, sorted((CSRC / "runtime").glob("*.cpp")), CSRC / "runtime", "_runtime", False, ("-lz", "-ltorch_python")),
+    ]
+    for out, srcs, hdr_dir, name, device, extra in targets:
+        headers = list(hdr_dir.glob("*.h")) + list((CSRC / "kernels").glob("*.h"))
+        flags = _common_flags(name)
+        objs, work = [], []
+        for s in srcs:
+            o = BUILD / f"{name}_{s.stem}.o"
+            objs.append(o)
+            if force or _needs(o, s, headers):
+                work.append((s, o))
+        if work:
+            with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+                futs = [ex.submit(_compile, s, o, flags, device) for s, o in work]
+                for f in futs:
+                    o = f.result()
+                    if verbose:
+                        print(f"[build] compiled {o.name}", flush=True)
+        if work or force or not out.exists() or any(o.stat().st_mtime > out.stat().st_mtime for o in objs):
+            _link(objs, out, device, extra)
+            if verbose:
+                print(f"[build] linked {out.relative_to(ROOT)}", flush=True)
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("-j", "--jobs", type=int, default=0)
+    ap.add_argument("--force", action="store_true")
+    a = ap.parse_args(argv)
+    build(a.jobs, a.force)
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,306 @@
+"""Autograd functions of the transformer hot path.
+
+GPU tensors run the hand-written gfx950 kernels in ``csrc/kernels`` (loaded by
+:func:`fault_tolerant_llm_training_amd._native.kernels`, which raises if the
+library is missing) and hipBLASLt GEMMs through ``torch.mm``/``torch.addmm``.
+CPU tensors run a pure-PyTorch reference of the same math (the CPU backend for
+the gloo tests); its backward recomputes the forward under autograd.
+
+Weight gradients never go through ``AccumulateGrad``: each function writes
+them into the parameter's :class:`GradSink` (a view of the flat gradient
+buffer) and returns ``None`` for the weight.
+
+Reference parity (math): RMSNorm model.py:24-48, RoPE model.py:100-126,
+attention model.py:179-215, SwiGLU model.py:253-254, embedding model.py:373,
+LM head model.py:379, loss train.py:101-102.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.nn.functional as F
+
+from .._native import kernels
+from .grad_sink import GradSink
+
+IGNORE_INDEX = -100
+
+
+def _write_weight_grad(sink: Optional[GradSink], g: torch.Tensor):
+    """CPU helper: route a computed weight gradient into its sink (or return it)."""
+    if sink is None:
+        return g
+    sink.set_(g.to(sink.buf.dtype))
+    return None
+
+
+# --------------------------------------------------------------------------------------
+# Embedding
+# --------------------------------------------------------------------------------------
+class EmbeddingFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, tokens, weight, sink):
+        ctx.sink = sink
+        ctx.vocab = weight.shape[0]
+        ctx.save_for_backward(tokens)
+        ctx.wshape = weight.shape
+        if weight.is_cuda:
+            return kernels().embedding_fwd(tokens.contiguous(), weight)
+        return F.embedding(tokens, weight)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (tokens,) = ctx.saved_tensors
+        sink = ctx.sink
+        dy = dy.contiguous()
+        if dy.is_cuda:
+            if sink is None:
+                dw = torch.zeros(ctx.wshape, dtype=dy.dtype, device=dy.device)
+                kernels().embedding_bwd_(dy, tokens.contiguous(), dw, False)
+                return None, dw, None
+            kernels().embedding_bwd_(dy, tokens.contiguous(), sink.buf, sink.accumulate)
+            sink.ready()
+            return None, None, None
+        dw = torch.zeros(ctx.wshape, dtype=torch.float32, device=dy.device)
+        dw.index_add_(0, tokens.reshape(-1), dy.reshape(-1, ctx.wshape[1]).float())
+        return None, _write_weight_grad(sink, dw.to(dy.dtype)), None
+
+
+def embedding(tokens, weight, sink=None):
+    return EmbeddingFn.apply(tokens, weight, sink)
+
+
+# --------------------------------------------------------------------------------------
+# RMSNorm / LayerNorm (weight only)
+# --------------------------------------------------------------------------------------
+def norm_reference(x: torch.Tensor, w: torch.Tensor, eps: float, layernorm: bool) -> torch.Tensor:
+    xf = x.float()
+    if layernorm:
+        xf = xf - xf.mean(-1, keepdim=True)
+    n = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps)
+    return n.type_as(x) * w
+
+
+class NormFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, sink, eps, layernorm):
+        ctx.sink, ctx.eps, ctx.ln = sink, eps, layernorm
+        if x.is_cuda:
+            xc = x.contiguous()
+            y, rstd, mean = kernels().norm_fwd(xc, weight, eps, layernorm)
+            ctx.save_for_backward(xc, weight, rstd, mean)
+            return y
+        ctx.save_for_backward(x, weight)
+        return norm_reference(x, weight, eps, layernorm)
+
+    @staticmethod
+    def backward(ctx, dy):
+        sink = ctx.sink
+        if dy.is_cuda:
+            x, w, rstd, mean = ctx.saved_tensors
+            if sink is not None:
+                dx = kernels().norm_bwd(dy.contiguous(), x, w, rstd, mean, sink.buf, None, sink.accumulate)
+                sink.ready()
+                return dx, None, None, None, None
+            dw = torch.empty_like(w)
+            dx = kernels().norm_bwd(dy.contiguous(), x, w, rstd, mean, dw, None, False)
+            return dx, dw, None, None, None
+        x, w = ctx.saved_tensors
+        with torch.enable_grad():
+            xr = x.detach().requires_grad_(True)
+            wr = w.detach().requires_grad_(True)
+            y = norm_reference(xr, wr, ctx.eps, ctx.ln)
+            dx, dw = torch.autograd.grad(y, (xr, wr), dy)
+        return dx, _write_weight_grad(sink, dw), None, None, None
+
+
+def norm(x, weight, sink=None, eps: float = 1e-5, layernorm: bool = False):
+    return NormFn.apply(x, weight, sink, eps, layernorm)
+
+
+# --------------------------------------------------------------------------------------
+# Linear (+ fused residual add through the GEMM's C input)
+# --------------------------------------------------------------------------------------
+class LinearFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, sink, residual):
+        K = x.shape[-1]
+        N = weight.shape[0]
+        x2 = x.reshape(-1, K)
+        if residual is None:
+            y = torch.mm(x2, weight.t())
+        else:
+            y = torch.addmm(residual.reshape(-1, N), x2, weight.t())
+        ctx.sink = sink
+        ctx.has_res = residual is not None
+        ctx.xshape = x.shape
+        ctx.save_for_backward(x2, weight)
+        return y.view(*x.shape[:-1], N)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w = ctx.saved_tensors
+        N = w.shape[0]
+        dy2 = dy.reshape(-1, N)
+        dw = None
+        # weight gradient first, so its all-reduce bucket can launch while dx runs
+        if ctx.sink is not None:
+            ctx.sink.mm(dy2.t(), x2)
+        else:
+            dw = torch.mm(dy2.t(), x2)
+        dx = torch.mm(dy2, w).view(ctx.xshape)
+        return dx, dw, None, (dy if ctx.has_res else None)
+
+
+def linear(x, weight, sink=None, residual=None):
+    return LinearFn.apply(x, weight, sink, residual)
+
+
+# --------------------------------------------------------------------------------------
+# RoPE + causal GQA attention on the fused QKV projection
+# --------------------------------------------------------------------------------------
+def rope_reference(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor) -> torch.Tensor:
+    """x: [B, S, H, D] interleaved pairs; cos/sin: [S, D/2] fp32."""
+    xf = x.float().reshape(*x.shape[:-1], -1, 2)
+    a, b = xf[..., 0], xf[..., 1]
+    c = cos[: x.shape[1]].view(1, x.shape[1], 1, -1)
+    s = sin[: x.shape[1]].view(1, x.shape[1], 1, -1)
+    out = torch.stack((a * c - b * s, a * s + b * c), dim=-1).flatten(-2)
+    return out.type_as(x)
+
+
+def attention_reference(qkv, cos, sin, seq_len, hq, hkv, d):
+    """Reference math: RoPE → repeat_kv → causal SDPA (model.py:179-215). qkv: [B*S, W]."""
+    T = qkv.shape[0]
+    B = T // seq_len
+    q = qkv[:, : hq * d].reshape(B, seq_len, hq, d)
+    k = qkv[:, hq * d : (hq + hkv) * d].reshape(B, seq_len, hkv, d)
+    v = qkv[:, (hq + hkv) * d :].reshape(B, seq_len, hkv, d)
+    q = rope_reference(q, cos, sin)
+    k = rope_reference(k, cos, sin)
+    rep = hq // hkv
+    if rep > 1:
+        k = k.repeat_interleave(rep, dim=2)
+        v = v.repeat_interleave(rep, dim=2)
+    o = F.scaled_dot_product_attention(q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2), is_causal=True)
+    return o.transpose(1, 2).reshape(T, hq * d)
+
+
+class RopeAttentionFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qkv, cos, sin, seq_len, hq, hkv, d):
+        ctx.cfg = (seq_len, hq, hkv, d)
+        if qkv.is_cuda:
+            from .attention import flash_attn_fwd
+
+            qkv = qkv.contiguous()
+            qk = kernels().rope_fwd(qkv, cos, sin, seq_len, hq, hkv, d)
+            o, lse = flash_attn_fwd(qk, qkv, seq_len, hq, hkv, d)
+            ctx.save_for_backward(qkv, qk, o, lse, cos, sin)
+            return o
+        ctx.save_for_backward(qkv, cos, sin)
+        return attention_reference(qkv, cos, sin, seq_len, hq, hkv, d)
+
+    @staticmethod
+    def backward(ctx, do):
+        seq_len, hq, hkv, d = ctx.cfg
+        if do.is_cuda:
+            from .attention import flash_attn_bwd
+
+            qkv, qk, o, lse, cos, sin = ctx.saved_tensors
+            dqkv = flash_attn_bwd(do.contiguous(), qk, qkv, o, lse, seq_len, hq, hkv, d)
+            kernels().rope_bwd_(dqkv, cos, sin, seq_len, hq, hkv, d)
+            return dqkv, None, None, None, None, None, None
+        qkv, cos, sin = ctx.saved_tensors
+        with torch.enable_grad():
+            x = qkv.detach().requires_grad_(True)
+            o = attention_reference(x, cos, sin, seq_len, hq, hkv, d)
+            (dx,) = torch.autograd.grad(o, (x,), do)
+        return dx, None, None, None, None, None, None
+
+
+def rope_attention(qkv, cos, sin, seq_len, hq, hkv, d):
+    return RopeAttentionFn.apply(qkv, cos, sin, seq_len, hq, hkv, d)
+
+
+# --------------------------------------------------------------------------------------
+# SwiGLU on the fused [w1; w3] projection
+# --------------------------------------------------------------------------------------
+def swiglu_reference(gu: torch.Tensor) -> torch.Tensor:
+    g, u = gu.chunk(2, dim=-1)
+    return F.silu(g) * u
+
+
+class SwiGLUFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, gu):
+        ctx.save_for_backward(gu)
+        if gu.is_cuda:
+            return kernels().swiglu_fwd(gu.contiguous())
+        return swiglu_reference(gu)
+
+    @staticmethod
+    def backward(ctx, da):
+        (gu,) = ctx.saved_tensors
+        if da.is_cuda:
+            return kernels().swiglu_bwd(da.contiguous(), gu.contiguous())
+        with torch.enable_grad():
+            x = gu.detach().requires_grad_(True)
+            (dx,) = torch.autograd.grad(swiglu_reference(x), (x,), da)
+        return dx
+
+
+def swiglu(gu):
+    return SwiGLUFn.apply(gu)
+
+
+# --------------------------------------------------------------------------------------
+# LM head + cross-entropy (sum over tokens × 1/num_items)
+# --------------------------------------------------------------------------------------
+class LMHeadCrossEntropyFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, h, weight, sink, labels, inv_count):
+        D = h.shape[-1]
+        h2 = h.reshape(-1, D)
+        lab = labels.reshape(-1)
+        ctx.sink = sink
+        ctx.hshape = h.shape
+        if h.is_cuda:
+            logits = torch.mm(h2, weight.t())
+            loss_rows, lse = kernels().xent_fwd(logits, lab.contiguous(), IGNORE_INDEX)
+            loss = loss_rows.sum() * inv_count
+            ctx.save_for_backward(h2, weight, logits, lse, lab, inv_count)
+            return loss
+        logits = torch.mm(h2, weight.t())
+        loss = F.cross_entropy(logits.float(), lab, reduction="sum", ignore_index=IGNORE_INDEX) * inv_count
+        ctx.save_for_backward(h2, weight, lab, inv_count)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        sink = ctx.sink
+        if g.is_cuda:
+            h2, w, logits, lse, lab, inv_count = ctx.saved_tensors
+            gf = g.detach().float().reshape(1).contiguous()
+            kernels().xent_bwd_(logits, lab, lse, gf, inv_count.float().reshape(1).contiguous(), IGNORE_INDEX)
+            dlogits = logits  # overwritten in place
+            dw = None
+            if sink is not None:
+                sink.mm(dlogits.t(), h2)
+            else:
+                dw = torch.mm(dlogits.t(), h2)
+            dh = torch.mm(dlogits, w).view(ctx.hshape)
+            return dh, dw, None, None, None
+        h2, w, lab, inv_count = ctx.saved_tensors
+        with torch.enable_grad():
+            hr = h2.detach().requires_grad_(True)
+            wr = w.detach().requires_grad_(True)
+            logits = torch.mm(hr, wr.t())
+            loss = F.cross_entropy(logits.float(), lab, reduction="sum", ignore_index=IGNORE_INDEX) * inv_count
+            dh, dw = torch.autograd.grad(loss, (hr, wr), g)
+        return dh.view(ctx.hshape), _write_weight_grad(sink, dw), None, None, None
+
+
+def lm_head_cross_entropy(h, weight, labels, inv_count, sink=None):
+    return LMHeadCrossEntropyFn.apply(h, weight, sink, labels, inv_count)

@@ -1,0 +1,130 @@
+"""Process-group bootstrap: one process per GPU, RCCL data plane + gloo control plane.
+
+The reference is single-process (train.sh:5-7; LOCAL_RANK only picks the
+device, train.py:16). Here ranks come from torchrun (RANK/LOCAL_RANK/WORLD_SIZE)
+or Slurm (SLURM_PROCID/SLURM_LOCALID/SLURM_NTASKS). Two groups are created:
+
+* the default group on ``nccl`` (= RCCL on ROCm, over xGMI inside a node) for
+  gradient all-reduce — stream-ordered, never blocks the host;
+* a ``gloo`` CPU group for control-plane agreement (stop-signal consensus,
+  token counts, data-loader states, config checks), so a 4-byte vote never
+  forces a GPU synchronisation.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class DistInfo:
+    rank: int = 0
+    world_size: int = 1
+    local_rank: int = 0
+    device: torch.device = torch.device("cpu")
+    ctrl_group: Optional[object] = None  # gloo group (None when world_size == 1)
+
+    @property
+    def is_main(self) -> bool:
+        return self.rank == 0
+
+    @property
+    def distributed(self) -> bool:
+        return self.world_size > 1
+
+
+_INFO: Optional[DistInfo] = None
+
+
+def env_ranks():
+    env = os.environ
+    if "RANK" in env and "WORLD_SIZE" in env:
+        return int(env["RANK"]), int(env["WORLD_SIZE"]), int(env.get("LOCAL_RANK", 0))
+    if "SLURM_PROCID" in env and "SLURM_NTASKS" in env:
+        return int(env["SLURM_PROCID"]), int(env["SLURM_NTASKS"]), int(env.get("SLURM_LOCALID", 0))
+    return 0, 1, int(env.get("LOCAL_RANK", 0))
+
+
+def init_distributed(device_type: str = "cuda", timeout_s: int = 1800) -> DistInfo:
+    global _INFO
+    if _INFO is not None:
+        return _INFO
+    rank, world, local = env_ranks()
+    if device_type == "cuda":
+        torch.cuda.set_device(local)
+        device = torch.device("cuda", local)
+    else:
+        device = torch.device("cpu")
+    info = DistInfo(rank, world, local, device)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29500")
+        os.environ["RANK"], os.environ["WORLD_SIZE"] = str(rank), str(world)
+        timeout = datetime.timedelta(seconds=timeout_s)
+        if not dist.is_initialized():
+            if device_type == "cuda":
+                dist.init_process_group("nccl", timeout=timeout, device_id=device)
+            else:
+                dist.init_process_group("gloo", timeout=timeout)
+        info.ctrl_group = dist.new_group(backend="gloo", timeout=timeout) if device_type == "cuda" else dist.group.WORLD
+    _INFO = info
+    return info
+
+
+def get_info() -> DistInfo:
+    return _INFO if _INFO is not None else DistInfo()
+
+
+def ctrl_allreduce_max(value: int) -> int:
+    """Host-side MAX vote over the gloo control group (no GPU sync)."""
+    info = get_info()
+    if not info.distributed:
+        return value
+    t = torch.tensor([value], dtype=torch.int64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=info.ctrl_group)
+    return int(t.item())
+
+
+def ctrl_allreduce_sum(value: float) -> float:
+    info = get_info()
+    if not info.distributed:
+        return value
+    t = torch.tensor([value], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM, group=info.ctrl_group)
+    return float(t.item())
+
+
+def ctrl_all_gather_object(obj):
+    info = get_info()
+    if not info.distributed:
+        return [obj]
+    out = [None] * info.world_size
+    dist.all_gather_object(out, obj, group=info.ctrl_group)
+    return out
+
+
+def ctrl_broadcast_object(obj, src: int = 0):
+    info = get_info()
+    if not info.distributed:
+        return obj
+    box = [obj]
+    dist.broadcast_object_list(box, src=src, group=info.ctrl_group)
+    return box[0]
+
+
+def barrier():
+    info = get_info()
+    if info.distributed:
+        dist.barrier(group=info.ctrl_group)
+
+
+def destroy():
+    global _INFO
+    if dist.is_initialized():
+        dist.destroy_process_group()
+    _INFO = None

@@ -1,0 +1,169 @@
+"""Command-line surface.
+
+The 16 reference flags are kept byte-for-byte (names, types, defaults, help):
+reference ``utils.py:112-203`` (table in SURVEY.md §2.6). Everything after the
+``# --- additive flags ---`` marker is new and defaults to the reference's
+behaviour.
+"""
+from __future__ import annotations
+
+import argparse
+import os
+
+import torch
+
+PRECISION_STR_TO_DTYPE = {
+    "fp16": torch.float16,
+    "bf16": torch.bfloat16,
+    "fp32": torch.float32,
+    "fp64": torch.float64,
+}
+
+
+def workdir() -> str:
+    """``$WORKDIR`` (reference ``utils.py:11``)."""
+    return os.getenv("WORKDIR", "")
+
+
+def jobid() -> str | None:
+    """``$SLURM_JOB_ID`` (reference ``utils.py:12``; read at call time, not import time)."""
+    return os.environ.get("SLURM_JOB_ID")
+
+
+def build_parser() -> argparse.ArgumentParser:
+    wd = workdir()
+    parser = argparse.ArgumentParser()
+    parser.add_argument(
+        "--dataset",
+        type=str,
+        default="/capstor/store/cscs/ethz/large-sc/datasets/train_data.parquet",
+        help="Path to a parquet file containing a 'text' column with documents (`str`)",
+    )
+    parser.add_argument(
+        "--checkpoint-path",
+        type=str,
+        default=f"{wd}/checkpoints",
+        help="Path to a checkpoint file to save the model and optimizer state dicts",
+    )
+    parser.add_argument(
+        "--checkpoint-id",
+        type=str,
+        default="",
+        help="Path to a checkpoint file to save the model and optimizer state dicts",
+    )
+    parser.add_argument(
+        "--tokenizer-name-or-path",
+        type=str,
+        default="unsloth/Mistral-Nemo-Base-2407-bnb-4bit",
+        help="A path to a directory containing vocabulary files required by the tokenizer or the model id of a predefined tokenizer hosted inside a model repo on the Hugging Face Hub.",
+    )
+    parser.add_argument("--sequence-length", type=int, default=4096)
+    parser.add_argument("--batch-size", type=int, default=1)
+    parser.add_argument(
+        "--fused-optimizer",
+        action="store_true",
+        help="Set to fuse the optimizer for increased performance or not",
+    )
+    parser.add_argument("--learning-rate", type=float, default=1e-5)
+    parser.add_argument("--lr-warmup-steps", type=int, default=10)
+    parser.add_argument("--training-steps", type=int, default=1000)
+    parser.add_argument(
+        "--logging-frequency", type=int, default=5, help="Log every `--logging-frequency` steps"
+    )
+    parser.add_argument("--grad-max-norm", type=float, default=1)
+    parser.add_argument(
+        "--model-dtype",
+        type=str,
+        default="bf16",
+        help="Model dtype for parameters, gradients and optimizer states. Default: bf16",
+    )
+    parser.add_argument(
+        "--compile", action="store_true", help="Set to compile the model with `torch.compile`"
+    )
+    parser.add_argument(
+        "--raise-error",
+        action="store_true",
+        help="Set to raise an error in the training loop at the error_step parameter",
+    )
+    parser.add_argument(
+        "--error-step",
+        type=int,
+        default=100,
+        help="Step at which to raise an error if --raise-error is set",
+    )
+    # --- additive flags (not in the reference; defaults keep its behaviour) ---
+    parser.add_argument(
+        "--model",
+        type=str,
+        default="llama3-8b",
+        help="Architecture preset: llama3-8b (reference train.py:43-53), gpt2-small, gpt2-medium, tiny",
+    )
+    parser.add_argument(
+        "--vocab-size",
+        type=int,
+        default=0,
+        help="Override the vocabulary size (0: tokenizer's, or 131072 with --synthetic-data)",
+    )
+    parser.add_argument(
+        "--synthetic-data",
+        action="store_true",
+        help="Deterministic synthetic token stream instead of parquet+tokenizer (offline boxes)",
+    )
+    parser.add_argument(
+        "--iterable-dataset",
+        action="store_true",
+        help="Use the packing IterableParquetDataset (resumable mid-shard) instead of ParquetDataset",
+    )
+    parser.add_argument("--seed", type=int, default=1234, help="RNG seed for init and data")
+    parser.add_argument(
+        "--device", type=str, default="cuda", choices=["cuda", "cpu"], help="Run on GPU (default) or CPU"
+    )
+    parser.add_argument(
+        "--save-every",
+        type=int,
+        default=0,
+        help="Periodic asynchronous checkpoint every N steps (0 disables)",
+    )
+    parser.add_argument(
+        "--no-async-checkpoint",
+        action="store_true",
+        help="Write checkpoints synchronously (torch.save on the main thread)",
+    )
+    parser.add_argument(
+        "--optimizer-state-dtype",
+        type=str,
+        default="",
+        help="AdamW moment dtype (bf16/fp32); default = --model-dtype like the reference",
+    )
+    parser.add_argument(
+        "--dp-bucket-mb",
+        type=float,
+        default=256.0,
+        help="Gradient all-reduce bucket size in MiB (data parallel)",
+    )
+    parser.add_argument(
+        "--consensus-every",
+        type=int,
+        default=1,
+        help="Agree on pending stop signals across ranks every N steps",
+    )
+    parser.add_argument(
+        "--metrics-file", type=str, default="", help="Append per-step JSON metrics to this file"
+    )
+    parser.add_argument(
+        "--sbatch-script",
+        type=str,
+        default="",
+        help="Job script resubmitted on SIGUSR1 (default: $WORKDIR/train.sh)",
+    )
+    parser.add_argument(
+        "--activation-checkpointing",
+        action="store_true",
+        help="Recompute each block in backward (long sequences)",
+    )
+    return parser
+
+
+def get_args(argv=None) -> argparse.Namespace:
+    """Parse flags (reference ``utils.py:112-203``)."""
+    return build_parser().parse_args(argv)

@@ -1,0 +1,160 @@
+"""Numerics of every hand-written HIP kernel vs a plain PyTorch fp32 reference."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def K():
+    from fault_tolerant_llm_training_amd._native import kernels
+
+    return kernels()
+
+
+def rel(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+@pytest.mark.parametrize("M,N", [(1, 128), (7, 768), (2048, 4096), (33, 1024), (5, 8192)])
+@pytest.mark.parametrize("ln", [False, True])
+def test_norm(K, M, N, ln):
+    torch.manual_seed(0)
+    x = torch.randn(M, N, device="cuda").bfloat16()
+    w = (1 + 0.1 * torch.randn(N, device="cuda")).bfloat16()
+    dy = torch.randn(M, N, device="cuda").bfloat16()
+    y, rstd, mean = K.norm_fwd(x, w, 1e-5, ln)
+    xr = x.float().requires_grad_(True)
+    wr = w.float().requires_grad_(True)
+    xc = xr - xr.mean(-1, keepdim=True) if ln else xr
+    ref = xc * torch.rsqrt(xc.pow(2).mean(-1, keepdim=True) + 1e-5) * wr
+    assert rel(y, ref) < 1e-2
+    dw = torch.empty_like(w)
+    dx = K.norm_bwd(dy, x, w, rstd, mean if ln else None, dw, None, False)
+    gx, gw = torch.autograd.grad(ref, (xr, wr), dy.float())
+    assert rel(dx, gx) < 2e-2
+    assert rel(dw, gw) < 2e-2
+
+
+@pytest.mark.parametrize("B,S,hq,hkv,d", [(1, 64, 4, 2, 128), (2, 128, 8, 8, 64), (1, 2048, 32, 8, 128)])
+def test_rope(K, B, S, hq, hkv, d):
+    from fault_tolerant_llm_training_amd.models.llama import rope_tables
+    from fault_tolerant_llm_training_amd.ops.functional import rope_reference
+
+    cos, sin = rope_tables(d, S, 500000.0)
+    cos, sin = cos.cuda(), sin.cuda()
+    W = (hq + 2 * hkv) * d
+    qkv = torch.randn(B * S, W, device="cuda").bfloat16()
+    qk = K.rope_fwd(qkv, cos, sin, S, hq, hkv, d)
+    q = rope_reference(qkv[:, : hq * d].view(B, S, hq, d).float(), cos, sin).view(B * S, -1)
+    k = rope_reference(qkv[:, hq * d : (hq + hkv) * d].view(B, S, hkv, d).float(), cos, sin).view(B * S, -1)
+    assert rel(qk, torch.cat([q, k], 1)) < 1e-2
+    # backward is the transpose rotation: <R x, y> == <x, R^T y>
+    dq = torch.randn(B * S, W, device="cuda").bfloat16()
+    d2 = dq.clone()
+    K.rope_bwd_(d2, cos, sin, S, hq, hkv, d)
+    xr = qkv.float().requires_grad_(True)
+    qr = rope_reference(xr[:, : hq * d].view(B, S, hq, d), cos, sin).reshape(B * S, -1)
+    kr = rope_reference(xr[:, hq * d : (hq + hkv) * d].view(B, S, hkv, d), cos, sin).reshape(B * S, -1)
+    out = torch.cat([qr, kr, xr[:, (hq + hkv) * d :]], 1)
+    (g,) = torch.autograd.grad(out, (xr,), dq.float())
+    assert rel(d2, g) < 1e-2
+
+
+@pytest.mark.parametrize("T,F_", [(1, 64), (300, 1408), (2048, 14336)])
+def test_swiglu(K, T, F_):
+    gu = torch.randn(T, 2 * F_, device="cuda").bfloat16()
+    a = K.swiglu_fwd(gu)
+    x = gu.float().requires_grad_(True)
+    g, u = x.chunk(2, -1)
+    ref = F.silu(g) * u
+    assert rel(a, ref) < 1e-2
+    da = torch.randn(T, F_, device="cuda").bfloat16()
+    dgu = K.swiglu_bwd(da, gu)
+    (gx,) = torch.autograd.grad(ref, (x,), da.float())
+    assert rel(dgu, gx) < 1e-2
+
+
+@pytest.mark.parametrize("T,V", [(3, 1024), (64, 32000), (16, 131072)])
+def test_xent(K, T, V):
+    logits = (3 * torch.randn(T, V, device="cuda")).bfloat16()
+    labels = torch.randint(0, V, (T,), device="cuda")
+    labels[0] = -100
+    loss, lse = K.xent_fwd(logits, labels, -100)
+    ref = F.cross_entropy(logits.float(), labels, reduction="none", ignore_index=-100)
+    assert torch.allclose(loss, ref, atol=2e-3, rtol=1e-3)
+    n = (labels != -100).sum().item()
+    inv = torch.tensor([1.0 / n], device="cuda")
+    g = torch.tensor([2.0], device="cuda")
+    lg = logits.clone()
+    K.xent_bwd_(lg, labels, lse, g, inv, -100)
+    x = logits.float().requires_grad_(True)
+    l2 = F.cross_entropy(x, labels, reduction="sum", ignore_index=-100) / n * 2.0
+    (gx,) = torch.autograd.grad(l2, (x,))
+    assert rel(lg, gx) < 1e-2
+
+
+def test_embedding(K):
+    V, D, T = 1000, 256, 512
+    w = torch.randn(V, D, device="cuda").bfloat16()
+    tok = torch.randint(0, 50, (2, T // 2), device="cuda")  # many duplicates
+    out = K.embedding_fwd(tok, w)
+    assert torch.equal(out, w[tok])
+    dy = torch.randn(2, T // 2, D, device="cuda").bfloat16()
+    dw = torch.full((V, D), 7.0, device="cuda").bfloat16()
+    K.embedding_bwd_(dy, tok, dw, False)
+    ref = torch.zeros(V, D, device="cuda").index_add_(0, tok.reshape(-1), dy.reshape(-1, D).float())
+    assert rel(dw, ref) < 1e-2
+    dw2 = dw.clone()
+    K.embedding_bwd_(dy, tok, dw2, False)
+    assert torch.equal(dw, dw2)  # deterministic
+
+
+@pytest.mark.parametrize("state_dtype", [torch.bfloat16, torch.float32])
+def test_grad_norm_adamw(K, state_dtype):
+    from fault_tolerant_llm_training_amd.optim.adamw import _adamw_reference
+
+    n = 1 << 20
+    g = torch.randn(n, device="cuda").bfloat16()
+    p = torch.randn(n, device="cuda").bfloat16()
+    m = (0.1 * torch.randn(n, device="cuda")).to(state_dtype)
+    v = (0.01 * torch.rand(n, device="cuda")).to(state_dtype)
+    stats = torch.zeros(3, device="cuda")
+    K.grad_norm_(g, stats, 1.0)
+    ref_norm = g.float().norm().item()
+    assert math.isclose(stats[0].item(), ref_norm, rel_tol=1e-4)
+    assert math.isclose(stats[1].item(), 1.0 / (ref_norm + 1e-6), rel_tol=1e-4)
+    p1, m1, v1 = p.clone(), m.clone(), v.clone()
+    K.adamw_(p1, g, m1, v1, stats, 1e-3, 0.9, 0.999, 1e-8, 0.01, 3)
+    p2, m2, v2 = p.clone(), m.clone(), v.clone()
+    _adamw_reference(p2, g, m2, v2, stats, 1e-3, 0.9, 0.999, 1e-8, 0.01, 3)
+    assert rel(p1, p2) < 1e-3 and rel(m1, m2) < 1e-2 and rel(v1, v2) < 1e-2
+    # non-finite gradients skip the update
+    g[5] = float("inf")
+    K.grad_norm_(g, stats, 1.0)
+    assert stats[2].item() == 1.0
+    p3 = p.clone()
+    K.adamw_(p3, g, m.clone(), v.clone(), stats, 1e-3, 0.9, 0.999, 1e-8, 0.01, 3)
+    assert torch.equal(p3, p)
+
+
+def test_tiny_model_gpu_vs_cpu():
+    """Whole model on the HIP path vs the CPU reference path: loss and all grads."""
+    from fault_tolerant_llm_training_amd.models.llama import build_model, model_args_for
+
+    a = model_args_for("tiny", vocab_size=512, seq_len=64)
+    mg = build_model(a, "cuda", torch.bfloat16, seed=7)
+    mc = build_model(a, "cpu", torch.bfloat16, seed=7)
+    mc.load_state_dict({k: v.cpu() for k, v in mg.state_dict().items()})
+    tok = torch.randint(0, 512, (2, 64))
+    lab = torch.randint(0, 512, (2, 64))
+    lg = mg(tok.cuda(), lab.cuda())
+    lc = mc(tok, lab)
+    lg.backward()
+    lc.backward()
+    assert abs(lg.item() - lc.item()) < 2e-2
+    assert rel(mg.flat.grads.cpu(), mc.flat.grads) < 3e-2
