@@ -1,0 +1,668 @@
+// Causal GQA flash attention, forward + backward, for gfx950 (CDNA4).
+//
+// Replaces the reference's repeat_kv + transpose + F.scaled_dot_product_attention
+// (reference model.py:179-215). Inputs are read in place
+// from the packed projections:
+//   qk  [T, (Hq+Hkv)*D]   rotated Q and K (written by the RoPE kernel)
+//   qkv [T, (Hq+2Hkv)*D]  fused QKV projection; V columns start at (Hq+Hkv)*D
+// KV head = h / (Hq/Hkv) is indexed directly: no repeat_kv copy, no transposes.
+//
+// MFMA formulation (v_mfma_f32_32x32x16_bf16, wave64):
+//  forward, per wave 32 query rows, per 64-key tile:
+//    S^T = K Q^T   (A = K rows from LDS, B = Q^T held in VGPRs for the whole loop)
+//      -> the accumulator has the query on the lane and keys in registers, so the
+//         row max / row sum of the online softmax are in-lane + one lane^32 swap;
+//    O^T += V^T P^T (A = V^T through ds_read_b64_tr_b16 transposed LDS reads,
+//         B = P^T taken straight from the S^T accumulator registers, no LDS trip);
+//    the running O^T keeps the query on the lane too, so the rescale by
+//    exp(m_old - m_new) is a per-lane scalar multiply.
+//  backward (FA2 style), per block 128 keys of one (batch, q-head), 4 waves x 32
+//    keys, sweeping 32-row query slices from the causal diagonal:
+//    S = Q K^T, dP = dO V^T (A = Q / dO rows from LDS, B = K / V in VGPRs),
+//    P = exp2(S*c - lse2), dS = P (dP - delta);
+//    dV += P^T dO, dK += dS^T Q (A = P / dS straight from accumulators,
+//    B = dO / Q through transposed LDS reads);
+//    dQ += dS K over the block's 128 keys (dS staged once through LDS) with fp32
+//    atomics; dK/dV per q-head partials are folded over the GQA group and
+//    converted to bf16 by a finalize kernel.
+// LDS images use an XOR swizzle of 16-B chunks that is conflict-free both for
+// ds_read_b128 row reads and for the 4-row ds_read_b64_tr_b16 transposed reads
+// (cdna_hip_programming.md T2/T10). Block->tile mapping: heavy causal tiles are
+// launched first and the GQA siblings of one KV head share blockIdx % 8 (same
+// XCD L2 under round-robin dispatch; a speed choice only).
+#include "torch_utils.h"
+
+#include <utility>
+
+namespace {
+
+typedef __attribute__((address_space(3))) bf16x4_t lds_bf16x4_t;
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+// Compile-time loop: indices are constants before SROA runs, so register arrays
+// indexed inside stay in VGPRs (a pragma-unrolled loop is unrolled too late and
+// leaves them in scratch / promoted LDS).
+template <typename F, int... I>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+constexpr float LOG2E_F = 1.4426950408889634f;
+
+// Byte offset of 16-B chunk c of row r in a [rows][D] bf16 LDS image.
+template <int D>
+__device__ __forceinline__ int lds_off(int r, int c) {
+  if constexpr (D == 128) {
+    return r * 256 + 16 * (c ^ (((r & 3) << 2) | ((r >> 2) & 3)));
+  } else {
+    static_assert(D == 64, "head_dim must be 64 or 128");
+    const int R = r >> 1, C = 8 * (r & 1) + c;
+    return R * 256 + 16 * (C ^ (((R & 3) << 2) | ((R >> 2) & 3)));
+  }
+}
+
+// Inverse of lds_off: which (row, chunk) lives at 16-B slot P of the image.
+template <int D>
+__device__ __forceinline__ void lds_inv(int P, int& r, int& c) {
+  const int R = P >> 4, Cp = P & 15;
+  const int C = Cp ^ (((R & 3) << 2) | ((R >> 2) & 3));
+  if constexpr (D == 128) {
+    r = R;
+    c = C;
+  } else {
+    r = 2 * R + (C >> 3);
+    c = C & 7;
+  }
+}
+
+// LDS-DMA (global_load_lds_dwordx4): each lane moves 16 B to lds_base + lane * 16.
+__device__ __forceinline__ void glds16(const void* g, char* lds_base) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                   (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
+}
+
+template <int D>
+__device__ __forceinline__ bf16x8_t ld_row(const char* img, int r, int c) {
+  return *reinterpret_cast<const bf16x8_t*>(img + lds_off<D>(r, c));
+}
+
+__device__ __forceinline__ bf16x4_t ds_tr(const char* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)(p));
+}
+
+__device__ __forceinline__ bf16x8_t cat8(bf16x4_t a, bf16x4_t b) {
+  bf16x8_t r;
+  r[0] = a[0]; r[1] = a[1]; r[2] = a[2]; r[3] = a[3];
+  r[4] = b[0]; r[5] = b[1]; r[6] = b[2]; r[7] = b[3];
+  return r;
+}
+
+// Transposed operand fragment from a swizzled [rows][D] image: lane receives
+// column col0 + (lane & 31) of rows row0 + 4*hi + (0..3) (elements 0..3) and
+// row0 + 8 + 4*hi + (0..3) (elements 4..7) — the k order of an MFMA operand
+// built from a 32x32 accumulator's registers 8s..8s+7.
+template <int D>
+__device__ __forceinline__ bf16x8_t tr_frag(const char* img, int row0, int col0, int lane) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3, hi = lane >> 5;
+  const int col = col0 + 16 * (g & 1) + 4 * p;
+  const int r = row0 + 4 * hi + q;
+  const int sub = ((col >> 2) & 1) * 8;
+  const bf16x4_t a = ds_tr(img + lds_off<D>(r, col >> 3) + sub);
+  const bf16x4_t b = ds_tr(img + lds_off<D>(r + 8, col >> 3) + sub);
+  return cat8(a, b);
+}
+
+// Same for the unswizzled [keys][32 q] dS image (64-B rows; 4 rows = one bank row).
+__device__ __forceinline__ bf16x8_t tr_frag_ds(const char* img, int row0, int lane) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3, hi = lane >> 5;
+  const int col = 16 * (g & 1) + 4 * p;
+  const int r = row0 + 4 * hi + q;
+  const bf16x4_t a = ds_tr(img + r * 64 + col * 2);
+  const bf16x4_t b = ds_tr(img + (r + 8) * 64 + col * 2);
+  return cat8(a, b);
+}
+
+template <int OFF>
+__device__ __forceinline__ bf16x8_t cvt8(const f32x16_t& v) {
+  bf16x8_t r;
+  r[0] = (__bf16)v[OFF + 0]; r[1] = (__bf16)v[OFF + 1]; r[2] = (__bf16)v[OFF + 2]; r[3] = (__bf16)v[OFF + 3];
+  r[4] = (__bf16)v[OFF + 4]; r[5] = (__bf16)v[OFF + 5]; r[6] = (__bf16)v[OFF + 6]; r[7] = (__bf16)v[OFF + 7];
+  return r;
+}
+
+__device__ __forceinline__ f32x16_t mfma32(bf16x8_t a, bf16x8_t b, f32x16_t c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ void map_head(int hh, int Hq, int Hkv, int& h, int& kvh) {
+  // hh in [0, Hq) -> (h, kvh) so that the Hq/Hkv siblings of one KV head are
+  // Hkv block-ids apart (same XCD when Hkv == 8).
+  const int G = Hq / Hkv;
+  kvh = hh % Hkv;
+  h = kvh * G + hh / Hkv;
+}
+
+// ================================================================== forward
+template <int D>
+__global__ __launch_bounds__(256, 2) void flash_fwd_kernel(const bf16_t* __restrict__ qk,
+                                                           const bf16_t* __restrict__ qkv,
+                                                           bf16_t* __restrict__ out,
+                                                           float* __restrict__ lse2, int B, int S,
+                                                           int Hq, int Hkv, float sl2) {
+  constexpr int BM = 128, BN = 64, KS = D / 16, NDB = D / 32, DCH = D / 8;
+  constexpr int TILE = BN * D * 2;
+  constexpr int CPT = BN * DCH / 256;
+  __shared__ __attribute__((aligned(16))) char smem[4 * TILE];
+
+  const int nqt = (S + BM - 1) / BM;
+  const int per = B * Hq;
+  const int L = blockIdx.x;
+  const int qt = nqt - 1 - L / per;  // heaviest causal tiles first
+  const int rem = L % per;
+  const int b = rem / Hq;
+  int h, kvh;
+  map_head(rem % Hq, Hq, Hkv, h, kvh);
+
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, l32 = lane & 31, hi = lane >> 5;
+  const int q0 = qt * BM + wave * 32;
+  const int qrow = q0 + l32;
+  const long ldqk = (long)(Hq + Hkv) * D, ldv = (long)(Hq + 2 * Hkv) * D, ldo = (long)Hq * D;
+  const bf16_t* Qg = qk + (long)b * S * ldqk + (long)h * D;
+  const bf16_t* Kg = qk + (long)b * S * ldqk + (long)(Hq + kvh) * D;
+  const bf16_t* Vg = qkv + (long)b * S * ldv + (long)(Hq + Hkv + kvh) * D;
+
+  bf16x8_t qf[KS];
+  {
+    const long qr = min(qrow, S - 1);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+      qf[ks] = *reinterpret_cast<const bf16x8_t*>(Qg + qr * ldqk + ks * 16 + hi * 8);
+  }
+
+  const int kend = min((qt + 1) * BM, S);
+  const int ntiles = (kend + BN - 1) / BN;
+  u32x4 kr[CPT], vr[CPT];
+#define FWD_GLOAD(KT)                                                        \
+  static_for<CPT>([&](auto I) {                                              \
+    const int id = tid + I * 256, row = id / DCH, c = id % DCH;              \
+    const long key = min((KT) * BN + row, S - 1);                            \
+    kr[I] = *reinterpret_cast<const u32x4*>(Kg + key * ldqk + c * 8);        \
+    vr[I] = *reinterpret_cast<const u32x4*>(Vg + key * ldv + c * 8);         \
+  });
+#define FWD_SWRITE(BUF)                                                      \
+  static_for<CPT>([&](auto I) {                                              \
+    const int id = tid + I * 256, row = id / DCH, c = id % DCH;              \
+    char* kb_ = smem + (BUF) * 2 * TILE;                                     \
+    *reinterpret_cast<u32x4*>(kb_ + lds_off<D>(row, c)) = kr[I];             \
+    *reinterpret_cast<u32x4*>(kb_ + TILE + lds_off<D>(row, c)) = vr[I];      \
+  });
+
+  FWD_GLOAD(0)
+  FWD_SWRITE(0)
+  __syncthreads();
+
+  f32x16_t o[NDB];
+#pragma unroll
+  for (int db = 0; db < NDB; ++db)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[db][r] = 0.f;
+  float m = -INFINITY, l = 0.f;
+
+  for (int kt = 0; kt < ntiles; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < ntiles) {
+      FWD_GLOAD(kt + 1)
+    }
+    const char* kb = smem + cur * 2 * TILE;
+    const char* vb = kb + TILE;
+    const int k0 = kt * BN;
+    const bool v0 = k0 <= q0 + 31;       // wave-uniform: sub-tile 0 has an unmasked key
+    const bool v1 = k0 + 32 <= q0 + 31;  // sub-tile 1
+    if (v0) {
+      f32x16_t s[2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) s[j][r] = 0.f;
+        if (j == 0 || v1) {
+#pragma unroll
+          for (int ks = 0; ks < KS; ++ks)
+            s[j] = mfma32(ld_row<D>(kb, j * 32 + l32, 2 * ks + hi), qf[ks], s[j]);
+        }
+      }
+      float mx = -INFINITY;
+      const bool diag = k0 + BN - 1 > q0;  // some key may exceed some query of this wave
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          float x = s[j][r] * sl2;
+          if (j == 1 && !v1) x = -INFINITY;
+          if (diag) {
+            const int key = k0 + j * 32 + (r & 3) + 8 * (r >> 2) + 4 * hi;
+            if (key > qrow) x = -INFINITY;
+          }
+          s[j][r] = x;
+          mx = fmaxf(mx, x);
+        }
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mn = fmaxf(m, mx);
+      const float alpha = exp2f(m - mn);
+      m = mn;
+      float ls = 0.f;
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float p = exp2f(s[j][r] - mn);
+          ls += p;
+          s[j][r] = p;
+        }
+      const bf16x8_t pb00 = cvt8<0>(s[0]), pb01 = cvt8<8>(s[0]);
+      const bf16x8_t pb10 = cvt8<0>(s[1]), pb11 = cvt8<8>(s[1]);
+      l = l * alpha + ls;
+#pragma unroll
+      for (int db = 0; db < NDB; ++db)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[db][r] *= alpha;
+#pragma unroll
+      for (int db = 0; db < NDB; ++db) {
+        o[db] = mfma32(tr_frag<D>(vb, 0, db * 32, lane), pb00, o[db]);
+        o[db] = mfma32(tr_frag<D>(vb, 16, db * 32, lane), pb01, o[db]);
+      }
+      if (v1) {
+#pragma unroll
+        for (int db = 0; db < NDB; ++db) {
+          o[db] = mfma32(tr_frag<D>(vb, 32, db * 32, lane), pb10, o[db]);
+          o[db] = mfma32(tr_frag<D>(vb, 48, db * 32, lane), pb11, o[db]);
+        }
+      }
+    }
+    if (kt + 1 < ntiles) {
+      FWD_SWRITE(cur ^ 1)
+    }
+    __syncthreads();
+  }
+#undef FWD_GLOAD
+#undef FWD_SWRITE
+
+  l += __shfl_xor(l, 32, 64);
+  const float inv = 1.f / l;
+  if (qrow < S) {
+    bf16_t* orow = out + ((long)b * S + qrow) * ldo + (long)h * D;
+#pragma unroll
+    for (int db = 0; db < NDB; ++db)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        uint2 v;
+        v.x = pack2(o[db][4 * g + 0] * inv, o[db][4 * g + 1] * inv);
+        v.y = pack2(o[db][4 * g + 2] * inv, o[db][4 * g + 3] * inv);
+        *reinterpret_cast<uint2*>(orow + db * 32 + 8 * g + 4 * hi) = v;
+      }
+    if (hi == 0) lse2[((long)b * Hq + h) * S + qrow] = m + log2f(l);
+  }
+}
+
+// ================================================================== backward
+// delta[b,h,q] = sum_d dO * O   (one 16-lane group per (q, h) row, 8 bf16 per lane step)
+template <int D>
+__global__ __launch_bounds__(256) void flash_bwd_pre_kernel(const bf16_t* __restrict__ dO,
+                                                            const bf16_t* __restrict__ O,
+                                                            float* __restrict__ delta, int B,
+                                                            int S, int Hq) {
+  const long row = (blockIdx.x * 256L + threadIdx.x) >> 4;  // (token, head) pair
+  const int sub = threadIdx.x & 15;
+  const long nrows = (long)B * S * Hq;
+  float acc = 0.f;
+  if (row < nrows) {
+    const bf16_t* a = dO + row * D;
+    const bf16_t* c = O + row * D;
+    for (int d = sub * 8; d < D; d += 128) {
+      float x[8], y[8];
+      unpack8(*reinterpret_cast<const uint4*>(a + d), x);
+      unpack8(*reinterpret_cast<const uint4*>(c + d), y);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc += x[j] * y[j];
+    }
+  }
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+  if (sub == 0 && row < nrows) {
+    const long t = row / Hq;  // token = b*S + q
+    const int h = (int)(row % Hq);
+    const long bb = t / S, q = t % S;
+    delta[(bb * Hq + h) * S + q] = acc;
+  }
+}
+
+template <int D>
+__global__ __launch_bounds__(256, 1) void flash_bwd_kernel(
+    const bf16_t* __restrict__ dO, const bf16_t* __restrict__ qk, const bf16_t* __restrict__ qkv,
+    const float* __restrict__ lse2, const float* __restrict__ delta, float* __restrict__ dq_acc,
+    float* __restrict__ dk_part, float* __restrict__ dv_part, int B, int S, int Hq, int Hkv,
+    float sl2, float scale) {
+  constexpr int BK = 128, BQ = 32, KS = D / 16, NDB = D / 32, DCH = D / 8;
+  constexpr int KIMG = BK * D * 2;   // K image (keys x D)
+  constexpr int QIMG = BQ * D * 2;   // one Q or dO slice
+  constexpr int DSIMG = BK * BQ * 2; // dS image [keys][32 q]
+  __shared__ __attribute__((aligned(16))) char smem[KIMG + 4 * QIMG + DSIMG + 4 * BQ * 4];
+  char* kimg = smem;
+  char* qimg = smem + KIMG;                 // [2][QIMG]
+  char* doimg = qimg + 2 * QIMG;            // [2][QIMG]
+  char* dsimg = doimg + 2 * QIMG;
+  float* stat = reinterpret_cast<float*>(dsimg + DSIMG);  // [2][lse 32 | delta 32]
+
+  const int per = B * Hq;
+  const int L = blockIdx.x;
+  const int kt = L / per;  // key tile; kt = 0 has the most query slices -> launched first
+  const int rem = L % per;
+  const int b = rem / Hq;
+  int h, kvh;
+  map_head(rem % Hq, Hq, Hkv, h, kvh);
+
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, l32 = lane & 31, hi = lane >> 5;
+  const int kb0 = kt * BK;
+  const int kw = kb0 + wave * 32;  // this wave's first key
+  const long ldqk = (long)(Hq + Hkv) * D, ldv = (long)(Hq + 2 * Hkv) * D, ldo = (long)Hq * D;
+  const bf16_t* Qg = qk + (long)b * S * ldqk + (long)h * D;
+  const bf16_t* Kg = qk + (long)b * S * ldqk + (long)(Hq + kvh) * D;
+  const bf16_t* Vg = qkv + (long)b * S * ldv + (long)(Hq + Hkv + kvh) * D;
+  const bf16_t* dOg = dO + (long)b * S * ldo + (long)h * D;
+  const float* lseg = lse2 + ((long)b * Hq + h) * S;
+  const float* delg = delta + ((long)b * Hq + h) * S;
+
+  // K tile -> LDS (all 128 keys), V fragments of this wave's 32 keys -> VGPRs
+#pragma unroll
+  for (int i = 0; i < BK * DCH / 256; ++i) {
+    const int id = tid + i * 256, row = id / DCH, c = id % DCH;
+    const long key = min(kb0 + row, S - 1);
+    *reinterpret_cast<uint4*>(kimg + lds_off<D>(row, c)) =
+        *reinterpret_cast<const uint4*>(Kg + key * ldqk + c * 8);
+  }
+  bf16x8_t vf[KS];
+  {
+    const long key = min(kw + l32, S - 1);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+      vf[ks] = *reinterpret_cast<const bf16x8_t*>(Vg + key * ldv + ks * 16 + hi * 8);
+  }
+
+  const int qs0 = kb0 / BQ;
+  const int nqs = (S + BQ - 1) / BQ;
+  float4 st = make_float4(0.f, 0.f, 0.f, 0.f);
+  // Q / dO slices go global -> LDS by LDS-DMA: the swizzle is applied to the
+  // per-lane SOURCE address (the LDS side is lane-linear), no staging VGPRs.
+  constexpr int GPW = QIMG / 1024 / 4;  // glds instructions per wave per image
+#define BWD_GLDS(QS, BUF)                                                      \
+  {                                                                            \
+    static_for<GPW>([&](auto I) {                                              \
+      const int piece = wave * GPW + I;                                        \
+      int r, c;                                                                \
+      lds_inv<D>(piece * 64 + lane, r, c);                                     \
+      const long q = min((QS) * BQ + r, S - 1);                                \
+      glds16(Qg + q * ldqk + c * 8, qimg + (BUF) * QIMG + piece * 1024);       \
+      glds16(dOg + q * ldo + c * 8, doimg + (BUF) * QIMG + piece * 1024);      \
+    });                                                                        \
+    if (tid < 16) {                                                            \
+      const int q = (QS) * BQ + (tid & 7) * 4;                                 \
+      const float* src = (tid < 8) ? lseg : delg;                              \
+      st.x = q + 0 < S ? src[q + 0] : 0.f;                                     \
+      st.y = q + 1 < S ? src[q + 1] : 0.f;                                     \
+      st.z = q + 2 < S ? src[q + 2] : 0.f;                                     \
+      st.w = q + 3 < S ? src[q + 3] : 0.f;                                     \
+    }                                                                          \
+  }
+#define BWD_STAT(BUF)                                                          \
+  if (tid < 16)                                                                \
+    *reinterpret_cast<float4*>(stat + (BUF) * 64 + (tid < 8 ? 0 : 32) + (tid & 7) * 4) = st;
+
+  BWD_GLDS(qs0, 0)
+  BWD_STAT(0)
+  __syncthreads();
+
+  f32x16_t dk[NDB], dv[NDB];
+#pragma unroll
+  for (int db = 0; db < NDB; ++db)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dk[db][r] = dv[db][r] = 0.f;
+
+  constexpr int WPD = 4 / NDB;        // waves per d-block in the dQ stage
+  constexpr int KPW = BK / WPD;       // keys per wave in the dQ stage
+  const int qdb = wave % NDB, qkp = wave / NDB;
+  const int key = kw + l32;
+
+  for (int qs = qs0; qs < nqs; ++qs) {
+    const int cur = (qs - qs0) & 1;
+    const bool more = qs + 1 < nqs;
+    const char* qi = qimg + cur * QIMG;
+    const char* di = doimg + cur * QIMG;
+    const float* ls = stat + cur * 64;
+    const float* dl = ls + 32;
+    const int qb = qs * BQ;
+    const bool active = qb + BQ - 1 >= kw;  // wave-uniform
+    if (active) {
+      f32x16_t s, dp;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) s[r] = dp[r] = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        s = mfma32(ld_row<D>(qi, l32, 2 * ks + hi), ld_row<D>(kimg, wave * 32 + l32, 2 * ks + hi), s);
+        dp = mfma32(ld_row<D>(di, l32, 2 * ks + hi), vf[ks], dp);
+      }
+      // C layout: lane -> key (col), registers -> query rows
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const float4 lq = *reinterpret_cast<const float4*>(ls + 8 * g + 4 * hi);
+        const float4 dq = *reinterpret_cast<const float4*>(dl + 8 * g + 4 * hi);
+        const float lv[4] = {lq.x, lq.y, lq.z, lq.w};
+        const float dv4[4] = {dq.x, dq.y, dq.z, dq.w};
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const int r = 4 * g + t;
+          const int q = qb + 8 * g + 4 * hi + t;
+          float p = exp2f(s[r] * sl2 - lv[t]);
+          if (key > q || q >= S) p = 0.f;
+          dp[r] = p * (dp[r] - dv4[t]);
+          s[r] = p;
+        }
+      }
+      const bf16x8_t pa[2] = {cvt8<0>(s), cvt8<8>(s)};
+      const bf16x8_t da[2] = {cvt8<0>(dp), cvt8<8>(dp)};
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss)
+#pragma unroll
+        for (int db = 0; db < NDB; ++db) {
+          dv[db] = mfma32(pa[ss], tr_frag<D>(di, 16 * ss, db * 32, lane), dv[db]);
+          dk[db] = mfma32(da[ss], tr_frag<D>(qi, 16 * ss, db * 32, lane), dk[db]);
+        }
+      // dS -> LDS image [key][q] (4 x 8-B writes per lane)
+      char* row = dsimg + (wave * 32 + l32) * 64;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        uint2 v;
+        v.x = pack2(dp[4 * g + 0], dp[4 * g + 1]);
+        v.y = pack2(dp[4 * g + 2], dp[4 * g + 3]);
+        *reinterpret_cast<uint2*>(row + (8 * g + 4 * hi) * 2) = v;
+      }
+    } else {
+      char* row = dsimg + (wave * 32 + l32) * 64;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) *reinterpret_cast<uint2*>(row + (8 * g + 4 * hi) * 2) = make_uint2(0, 0);
+    }
+    __syncthreads();
+    if (more) BWD_GLDS(qs + 1, cur ^ 1)
+    // dQ[q, d] += scale * sum_keys dS[q, key] K[key, d]
+    {
+      f32x16_t acc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+      const int kbeg = qkp * KPW;
+      // skip key ranges that are entirely above the causal diagonal for this slice
+      if (kb0 + kbeg <= qb + BQ - 1) {
+#pragma unroll
+        for (int k2 = 0; k2 < KPW / 16; ++k2) {
+          const int kk = kbeg + 16 * k2;
+          acc = mfma32(tr_frag_ds(dsimg, kk, lane), tr_frag<D>(kimg, kk, qdb * 32, lane), acc);
+        }
+        const int d = qdb * 32 + l32;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int q = qb + (r & 3) + 8 * (r >> 2) + 4 * hi;
+          if (q < S) atomicAdd(dq_acc + ((long)b * S + q) * ldo + (long)h * D + d, acc[r] * scale);
+        }
+      }
+    }
+    if (more) BWD_STAT(cur ^ 1)
+    __syncthreads();
+  }
+#undef BWD_GLDS
+#undef BWD_STAT
+
+  // dK / dV partials of this q-head (C layout: lane -> d, registers -> keys)
+#pragma unroll
+  for (int db = 0; db < NDB; ++db)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int k = kw + (r & 3) + 8 * (r >> 2) + 4 * hi;
+      if (k < S) {
+        const long off = ((long)b * S + k) * ldo + (long)h * D + db * 32 + l32;
+        dk_part[off] = dk[db][r] * scale;
+        dv_part[off] = dv[db][r];
+      }
+    }
+}
+
+// dqkv[:, q | k | v] = bf16(dQ), bf16(sum_G dK_part), bf16(sum_G dV_part)
+__global__ __launch_bounds__(256) void flash_bwd_finalize_kernel(
+    const float* __restrict__ dq_acc, const float* __restrict__ dk_part,
+    const float* __restrict__ dv_part, bf16_t* __restrict__ dqkv, long T, int Hq, int Hkv, int D) {
+  const int G = Hq / Hkv;
+  const int W = (Hq + 2 * Hkv) * D;
+  const int vpr = W / 4;
+  const long total = T * vpr;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const long t = i / vpr;
+    const int col = (int)(i - t * vpr) * 4;
+    float4 v;
+    if (col < Hq * D) {
+      v = *reinterpret_cast<const float4*>(dq_acc + t * Hq * D + col);
+    } else {
+      const bool isk = col < (Hq + Hkv) * D;
+      const int c2 = col - (isk ? Hq * D : (Hq + Hkv) * D);
+      const int kh = c2 / D, d = c2 % D;
+      const float* src = (isk ? dk_part : dv_part) + t * Hq * D + (long)kh * G * D + d;
+      v = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int r = 0; r < G; ++r) {
+        const float4 x = *reinterpret_cast<const float4*>(src + r * D);
+        v.x += x.x; v.y += x.y; v.z += x.z; v.w += x.w;
+      }
+    }
+    uint2 o;
+    o.x = pack2(v.x, v.y);
+    o.y = pack2(v.z, v.w);
+    *reinterpret_cast<uint2*>(dqkv + t * W + col) = o;
+  }
+}
+
+void check_inputs(const at::Tensor& qk, const at::Tensor& qkv, int64_t S, int64_t Hq, int64_t Hkv,
+                  int64_t D) {
+  FT_CHECK_CUDA(qk);
+  FT_CHECK_BF16(qk);
+  FT_CHECK_BF16(qkv);
+  FT_CHECK_CONTIG(qk);
+  FT_CHECK_CONTIG(qkv);
+  TORCH_CHECK(D == 64 || D == 128, "flash: head_dim must be 64 or 128");
+  TORCH_CHECK(Hq % Hkv == 0, "flash: Hq must be a multiple of Hkv");
+  TORCH_CHECK(qk.size(-1) == (Hq + Hkv) * D, "flash: qk width");
+  TORCH_CHECK(qkv.size(-1) == (Hq + 2 * Hkv) * D, "flash: qkv width");
+  TORCH_CHECK(qk.size(0) == qkv.size(0) && qk.size(0) % S == 0, "flash: rows");
+}
+
+}  // namespace
+
+// Returns (o [T, Hq*D] bf16, lse2 [B, Hq, S] fp32; lse2 = log2 of the softmax denominator
+// in the exp2 domain, i.e. P = exp2(s * scale * log2e - lse2)).
+std::tuple<at::Tensor, at::Tensor> flash_fwd(const at::Tensor& qk, const at::Tensor& qkv,
+                                             int64_t S, int64_t Hq, int64_t Hkv, int64_t D) {
+  check_inputs(qk, qkv, S, Hq, Hkv, D);
+  const int T = qk.size(0);
+  const int B = T / S;
+  const at::DeviceGuard guard(qk.device());
+  auto out = at::empty({T, Hq * D}, qk.options());
+  auto lse = at::empty({B, Hq, S}, qk.options().dtype(at::kFloat));
+  const float sl2 = LOG2E_F / std::sqrt((float)D);
+  const int nqt = (S + 127) / 128;
+  dim3 grid(nqt * B * Hq), block(256);
+  if (D == 128)
+    hipLaunchKernelGGL(flash_fwd_kernel<128>, grid, block, 0, ft_stream(), cptr<bf16_t>(qk),
+                       cptr<bf16_t>(qkv), mptr<bf16_t>(out), mptr<float>(lse), B, (int)S, (int)Hq,
+                       (int)Hkv, sl2);
+  else
+    hipLaunchKernelGGL(flash_fwd_kernel<64>, grid, block, 0, ft_stream(), cptr<bf16_t>(qk),
+                       cptr<bf16_t>(qkv), mptr<bf16_t>(out), mptr<float>(lse), B, (int)S, (int)Hq,
+                       (int)Hkv, sl2);
+  FT_LAUNCH_CHECK();
+  return {out, lse};
+}
+
+// Returns dqkv [T, (Hq+2Hkv)*D] bf16 (dQ/dK in the rotated frame; RoPE backward follows).
+at::Tensor flash_bwd(const at::Tensor& dout, const at::Tensor& qk, const at::Tensor& qkv,
+                     const at::Tensor& out, const at::Tensor& lse, int64_t S, int64_t Hq,
+                     int64_t Hkv, int64_t D) {
+  check_inputs(qk, qkv, S, Hq, Hkv, D);
+  FT_CHECK_CONTIG(dout);
+  FT_CHECK_CONTIG(out);
+  const int T = qk.size(0);
+  const int B = T / S;
+  TORCH_CHECK(dout.numel() == (long)T * Hq * D && out.numel() == (long)T * Hq * D, "flash_bwd: o shape");
+  TORCH_CHECK(lse.numel() == (long)B * Hq * S, "flash_bwd: lse shape");
+  const at::DeviceGuard guard(qk.device());
+  auto f32 = qk.options().dtype(at::kFloat);
+  auto delta = at::empty({B, Hq, S}, f32);
+  auto dq_acc = at::zeros({T, Hq * D}, f32);
+  auto dk_part = at::empty({T, Hq * D}, f32);
+  auto dv_part = at::empty({T, Hq * D}, f32);
+  auto dqkv = at::empty({T, (Hq + 2 * Hkv) * D}, qk.options());
+  const float sl2 = LOG2E_F / std::sqrt((float)D);
+  const float scale = 1.f / std::sqrt((float)D);
+  const long rows = (long)T * Hq;
+  const int pre_blocks = (int)((rows * 16 + 255) / 256);
+  const int nkt = (S + 127) / 128;
+  dim3 grid(nkt * B * Hq), block(256);
+  if (D == 128) {
+    hipLaunchKernelGGL(flash_bwd_pre_kernel<128>, dim3(pre_blocks), block, 0, ft_stream(),
+                       cptr<bf16_t>(dout), cptr<bf16_t>(out), mptr<float>(delta), B, (int)S, (int)Hq);
+    hipLaunchKernelGGL(flash_bwd_kernel<128>, grid, block, 0, ft_stream(), cptr<bf16_t>(dout),
+                       cptr<bf16_t>(qk), cptr<bf16_t>(qkv), cptr<float>(lse), cptr<float>(delta),
+                       mptr<float>(dq_acc), mptr<float>(dk_part), mptr<float>(dv_part), B, (int)S,
+                       (int)Hq, (int)Hkv, sl2, scale);
+  } else {
+    hipLaunchKernelGGL(flash_bwd_pre_kernel<64>, dim3(pre_blocks), block, 0, ft_stream(),
+                       cptr<bf16_t>(dout), cptr<bf16_t>(out), mptr<float>(delta), B, (int)S, (int)Hq);
+    hipLaunchKernelGGL(flash_bwd_kernel<64>, grid, block, 0, ft_stream(), cptr<bf16_t>(dout),
+                       cptr<bf16_t>(qk), cptr<bf16_t>(qkv), cptr<float>(lse), cptr<float>(delta),
+                       mptr<float>(dq_acc), mptr<float>(dk_part), mptr<float>(dv_part), B, (int)S,
+                       (int)Hq, (int)Hkv, sl2, scale);
+  }
+  FT_LAUNCH_CHECK();
+  const long vec = (long)T * ((Hq + 2 * Hkv) * D / 4);
+  const int fin_blocks = (int)std::max(1L, std::min((vec + 255) / 256, 4096L));
+  hipLaunchKernelGGL(flash_bwd_finalize_kernel, dim3(fin_blocks), block, 0, ft_stream(),
+                     cptr<float>(dq_acc), cptr<float>(dk_part), cptr<float>(dv_part),
+                     mptr<bf16_t>(dqkv), (long)T, (int)Hq, (int)Hkv, (int)D);
+  FT_LAUNCH_CHECK();
+  return dqkv;
+}
+
+TORCH_LIBRARY_FRAGMENT(ftamd, m) {
+  m.def("flash_fwd(Tensor qk, Tensor qkv, int S, int Hq, int Hkv, int D) -> (Tensor, Tensor)",
+        &flash_fwd);
+  m.def(
+      "flash_bwd(Tensor dout, Tensor qk, Tensor qkv, Tensor out, Tensor lse, int S, int Hq, int "
+      "Hkv, int D) -> Tensor",
+      &flash_bwd);
+}

@@ -67,7 +67,7 @@ PRESETS = {
                        rope_theta=10000),
     "gpt2-medium": dict(dim=1024, n_layers=24, n_heads=16, n_kv_heads=16, multiple_of=256,
                         rope_theta=10000),
-    "tiny": dict(dim=128, n_layers=2, n_heads=4, n_kv_heads=2, multiple_of=64, rope_theta=10000),
+    "tiny": dict(dim=256, n_layers=2, n_heads=4, n_kv_heads=2, multiple_of=64, rope_theta=10000),
 }
 
 

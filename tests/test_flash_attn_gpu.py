@@ -1,0 +1,60 @@
+"""HIP flash attention (fwd + bwd) vs an fp32 PyTorch reference (repeat_kv + causal softmax)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def ref_attn(q, k, v):
+    """q [B,S,Hq,D], k/v [B,S,Hkv,D] fp32 -> o [B,S,Hq,D]."""
+    B, S, Hq, D = q.shape
+    rep = Hq // k.shape[2]
+    k = k.repeat_interleave(rep, 2)
+    v = v.repeat_interleave(rep, 2)
+    s = torch.einsum("bqhd,bkhd->bhqk", q, k) / D**0.5
+    mask = torch.ones(S, S, dtype=torch.bool, device=q.device).triu(1)
+    s = s.masked_fill(mask, float("-inf"))
+    p = s.softmax(-1)
+    return torch.einsum("bhqk,bkhd->bqhd", p, v)
+
+
+def rel(a, b):
+    return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
+
+
+@pytest.mark.parametrize(
+    "B,S,Hq,Hkv,D",
+    [(1, 128, 2, 1, 128), (1, 256, 4, 2, 128), (2, 192, 4, 4, 64), (1, 2048, 32, 8, 128), (1, 320, 8, 2, 64),
+     (2, 512, 12, 12, 64)],
+)
+def test_flash_fwd_bwd(B, S, Hq, Hkv, D):
+    from fault_tolerant_llm_training_amd._native import kernels
+
+    K = kernels()
+    torch.manual_seed(0)
+    T = B * S
+    qkv = torch.randn(T, (Hq + 2 * Hkv) * D, device="cuda").bfloat16()
+    qk = torch.randn(T, (Hq + Hkv) * D, device="cuda").bfloat16()
+    o, lse = K.flash_fwd(qk, qkv, S, Hq, Hkv, D)
+    q = qk[:, : Hq * D].float().view(B, S, Hq, D).requires_grad_(True)
+    k = qk[:, Hq * D :].float().view(B, S, Hkv, D).requires_grad_(True)
+    v = qkv[:, (Hq + Hkv) * D :].float().view(B, S, Hkv, D).requires_grad_(True)
+    ref = ref_attn(q, k, v)
+    assert rel(o.view(B, S, Hq, D), ref) < 1e-2
+    do = torch.randn(T, Hq * D, device="cuda").bfloat16()
+    dqkv = K.flash_bwd(do, qk, qkv, o, lse, S, Hq, Hkv, D)
+    gq, gk, gv = torch.autograd.grad(ref, (q, k, v), do.float().view(B, S, Hq, D))
+    assert rel(dqkv[:, : Hq * D].view(B, S, Hq, D), gq) < 2e-2
+    assert rel(dqkv[:, Hq * D : (Hq + Hkv) * D].view(B, S, Hkv, D), gk) < 2e-2
+    assert rel(dqkv[:, (Hq + Hkv) * D :].view(B, S, Hkv, D), gv) < 2e-2
+
+
+def test_flash_deterministic_fwd():
+    from fault_tolerant_llm_training_amd._native import kernels
+
+    K = kernels()
+    qkv = torch.randn(1024, 48 * 128, device="cuda").bfloat16()
+    qk = torch.randn(1024, 40 * 128, device="cuda").bfloat16()
+    o1, _ = K.flash_fwd(qk, qkv, 1024, 32, 8, 128)
+    o2, _ = K.flash_fwd(qk, qkv, 1024, 32, 8, 128)
+    assert torch.equal(o1, o2)
