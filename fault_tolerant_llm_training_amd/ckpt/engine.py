@@ -1,0 +1,252 @@
+"""Asynchronous checkpoint engine: HBM snapshot → pinned host → parallel file writer.
+
+The reference saves with a synchronous ``torch.save`` of CUDA tensors (reference
+``utils.py:74-80``): a pageable D2H per tensor inside pickling, then a
+single-threaded write straight to the final path — ≈33.6 s for the 48 GB
+Llama-3-8B state, during which training is stopped.
+
+Here the whole training state is three flat HBM buffers (parameters,
+``exp_avg``, ``exp_avg_sq``), so a checkpoint is three big DMA copies:
+
+1. ``snapshot`` — on a dedicated HIP stream that first waits for the compute
+   stream (event), copy the buffers into a reserved HBM staging area
+   (``mode="hbm"``: 48 GB at HBM3E speed ≈ 20 ms; MI355X's 288 GB holds the
+   64 GB of training state plus this copy), or directly into pinned host memory
+   (``mode="host"``). The compute stream is made to wait for the snapshot event
+   only right before the next optimizer step would overwrite the state
+   (:meth:`fence`), so forward/backward of the next step overlap the copy.
+2. ``drain`` — D2H of the staging copy into exact-size pinned host buffers
+   (``hipHostMalloc``) on the same side stream; training never waits for it.
+3. ``write`` — the native :class:`ZipWriter` thread waits for the drain event,
+   then CRCs and ``pwrite``s 64 MiB chunks with a thread pool, fsyncs and
+   atomically renames the file into place.
+
+CPU tensors (tests, ``--device cpu``) take the same path with a synchronous
+host copy. Without the native runtime the writer falls back to ``torch.save``
+(temp file + fsync + rename) on a Python thread.
+"""
+from __future__ import annotations
+
+import os
+import threading
+import time
+from dataclasses import dataclass, field
+from typing import Any, Callable, Dict, List, Optional
+
+import torch
+
+from .._native import runtime, runtime_available
+from .format import ARCHIVE, archive_records, write_archive_python
+
+
+@dataclass
+class SaveStats:
+    path: str = ""
+    step: int = -1
+    mode: str = ""
+    bytes: int = 0
+    snapshot_s: float = 0.0      # host time to enqueue the snapshot (+ its completion when blocking)
+    stall_s: float = 0.0         # time the training loop was blocked by this save
+    drain_wait_s: float = 0.0    # writer thread waiting for the D2H drain
+    write_s: float = 0.0         # CRC + pwrite
+    fsync_s: float = 0.0         # fsync + rename (+ dir fsync)
+    total_s: float = 0.0         # save() call → file durable
+    error: str = ""
+
+    def as_dict(self) -> Dict[str, Any]:
+        return dict(self.__dict__)
+
+
+@dataclass
+class _InFlight:
+    stats: SaveStats
+    t0: float
+    writer: Any = None                    # native ZipWriter
+    thread: Optional[threading.Thread] = None  # python fallback writer
+    keep: List[Any] = field(default_factory=list)  # host tensors referenced by the writer
+    done: bool = False
+
+
+class CheckpointEngine:
+    def __init__(self, buffers: Dict[str, torch.Tensor], mode: str = "auto", writer_threads: int = 8,
+                 fsync: bool = True, hbm_headroom_gb: float = 16.0):
+        """``buffers``: name → flat device (or CPU) tensor holding training state."""
+        self.buffers = dict(buffers)
+        self.device = next(iter(self.buffers.values())).device
+        self.is_cuda = self.device.type == "cuda"
+        self.native = runtime_available()
+        self.writer_threads = writer_threads
+        self.fsync = fsync
+        self.nbytes = sum(b.numel() * b.element_size() for b in self.buffers.values())
+        if mode == "auto":
+            mode = "cpu"
+            if self.is_cuda:
+                free, _total = torch.cuda.mem_get_info(self.device)
+                mode = "hbm" if free > self.nbytes + hbm_headroom_gb * 2**30 else "host"
+        if not self.is_cuda:
+            mode = "cpu"
+        self.mode = mode
+        self._host: Optional[Dict[str, torch.Tensor]] = None
+        self._stage: Optional[Dict[str, torch.Tensor]] = None
+        self._eng = None
+        self._snap_ev: Optional[int] = None
+        self._inflight: Optional[_InFlight] = None
+        self.history: List[SaveStats] = []
+
+    # ------------------------------------------------------------------ buffers
+    def _ensure_host(self) -> Dict[str, torch.Tensor]:
+        if self._host is None:
+            host = {}
+            for k, b in self.buffers.items():
+                nb = b.numel() * b.element_size()
+                if self.is_cuda and self.native:
+                    raw = runtime().pinned_empty(nb)  # exact size (torch's pinned pool rounds to 2^k)
+                elif self.is_cuda:
+                    raw = torch.empty(nb, dtype=torch.uint8, pin_memory=True)
+                else:
+                    raw = torch.empty(nb, dtype=torch.uint8)
+                host[k] = raw.view(b.dtype)
+            self._host = host
+        return self._host
+
+    def _ensure_stage(self) -> Dict[str, torch.Tensor]:
+        if self._stage is None:
+            self._stage = {k: torch.empty_like(b) for k, b in self.buffers.items()}
+        return self._stage
+
+    def preallocate(self) -> None:
+        """Allocate pinned host (and HBM staging) buffers ahead of the first save."""
+        self._ensure_host()
+        if self.mode == "hbm":
+            self._ensure_stage()
+
+    def host_views(self) -> Dict[str, torch.Tensor]:
+        return self._ensure_host()
+
+    # ------------------------------------------------------------------ snapshot
+    def _snapshot(self) -> Optional[int]:
+        """Enqueue the copies; returns the native event index the writer must wait on."""
+        host = self._ensure_host()
+        if not self.is_cuda:
+            for k, b in self.buffers.items():
+                host[k].copy_(b)
+            return None
+        if not self.native:
+            # no native engine: synchronous pinned copies on the current stream
+            for k, b in self.buffers.items():
+                host[k].copy_(b, non_blocking=True)
+            torch.cuda.current_stream(self.device).synchronize()
+            return None
+        rt = runtime()
+        if self._eng is None:
+            self._eng = rt.SnapshotEngine(self.device.index or 0)
+        eng = self._eng
+        eng.begin(torch.cuda.current_stream(self.device).cuda_stream)
+        if self.mode == "hbm":
+            stage = self._ensure_stage()
+            for k, b in self.buffers.items():
+                eng.copy(stage[k].data_ptr(), b.data_ptr(), b.numel() * b.element_size())
+            self._snap_ev = eng.mark()
+            src = stage
+        else:
+            src = self.buffers
+        for k, b in src.items():
+            eng.copy(host[k].data_ptr(), b.data_ptr(), b.numel() * b.element_size())
+        drained = eng.mark()
+        if self.mode != "hbm":
+            self._snap_ev = drained
+        return drained
+
+    def fence(self) -> None:
+        """Make the compute stream wait for the pending snapshot (call before optimizer.step)."""
+        if self._snap_ev is not None and self._eng is not None:
+            if not self._eng.query(self._snap_ev):
+                self._eng.stream_wait(torch.cuda.current_stream(self.device).cuda_stream, self._snap_ev)
+            self._snap_ev = None
+
+    # ------------------------------------------------------------------ save
+    def save(self, path: str, build_state: Callable[[Dict[str, torch.Tensor]], Any], step: int = -1,
+             blocking: bool = False) -> SaveStats:
+        """Snapshot the buffers and write ``build_state(host_views)`` to ``path``.
+
+        ``build_state`` receives the host buffers (same keys as ``buffers``) and
+        returns the object to serialise; its tensors must be views of them (or
+        small CPU tensors). Returns immediately unless ``blocking``.
+        """
+        t0 = time.perf_counter()
+        self.wait()  # host buffers are reused: the previous file must be on disk
+        st = SaveStats(path=path, step=step, mode=self.mode, bytes=self.nbytes)
+        os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
+        ev = self._snapshot()
+        obj = build_state(self._ensure_host())
+        inf = _InFlight(stats=st, t0=t0)
+        tmp = path + ".tmp"
+        if self.native:
+            rt = runtime()
+            small, storages = archive_records(obj)
+            w = rt.ZipWriter(tmp, path, ARCHIVE, self.writer_threads)
+            for name, data in small[:4]:
+                w.add_bytes(name, data)
+            for key, storage in storages:
+                w.add_buffer(f"data/{key}", storage.data_ptr(), storage.nbytes())
+                inf.keep.append(storage)
+            for name, data in small[4:]:
+                w.add_bytes(name, data)
+            handle = self._eng.event_handle(ev) if (ev is not None and self._eng is not None) else 0
+            w.start(handle, self.fsync)
+            inf.writer = w
+            st.bytes = w.total_size()
+        else:
+            def _py_write():
+                try:
+                    st.bytes = write_archive_python(obj, path, self.fsync)
+                except Exception as e:  # pragma: no cover - reported through stats
+                    st.error = repr(e)
+
+            inf.thread = threading.Thread(target=_py_write, name="ft-ckpt-writer", daemon=True)
+            inf.thread.start()
+            inf.keep.append(obj)
+        st.snapshot_s = time.perf_counter() - t0
+        self._inflight = inf
+        if blocking:
+            if self.is_cuda and self._snap_ev is not None:
+                self.fence()
+            self.wait()
+        st.stall_s = time.perf_counter() - t0 if blocking else st.snapshot_s
+        return st
+
+    def poll(self) -> Optional[SaveStats]:
+        """Non-blocking: if the in-flight save finished, retire it and return its stats."""
+        inf = self._inflight
+        if inf is None:
+            return None
+        if inf.writer is not None and not inf.writer.done():
+            return None
+        if inf.thread is not None and inf.thread.is_alive():
+            return None
+        return self.wait()
+
+    def wait(self) -> Optional[SaveStats]:
+        """Block until the in-flight save (if any) is durable; returns its stats."""
+        inf = self._inflight
+        if inf is None:
+            return None
+        st = inf.stats
+        if inf.writer is not None:
+            ws = inf.writer.wait()
+            st.drain_wait_s, st.write_s, st.fsync_s = ws.wait_seconds, ws.write_seconds, ws.fsync_seconds
+            st.bytes = ws.bytes or st.bytes
+            if ws.error:
+                st.error = ws.error
+        if inf.thread is not None:
+            inf.thread.join()
+        st.total_s = time.perf_counter() - inf.t0
+        self._inflight = None
+        self.history.append(st)
+        if st.error:
+            raise RuntimeError(f"checkpoint write to {st.path} failed: {st.error}")
+        return st
+
+    @property
+    def busy(self) -> bool:
+        return self._inflight is not None

@@ -9,7 +9,9 @@ Behavioural parity with the reference:
   ``inputs = ids[:, :-1]``, ``labels = ids[:, 1:]`` with pad labels → ``-100``.
 * :class:`IterableParquetDataset` — reference ``dataset.py:56-101``: packs
   successive documents into ``S+1`` tokens, re-reads the last (truncated)
-  document for the next sample, masks labels at / after BOS.
+  document for the next sample, masks labels at / after BOS. One fix: a
+  document that alone fills a sample is not re-read (the reference would
+  repeat it forever).
 
 Additions: both datasets expose ``state_dict()`` /
 ``load_state_dict()`` so a resumed job seeks in O(1) instead of re-tokenizing
@@ -115,12 +117,18 @@ class IterableParquetDataset(torch.utils.data.IterableDataset):
     def __next__(self):
         S1 = self.sequence_length + 1
         buf: List[int] = []
+        docs = 0
         while len(buf) < S1:
             buf.extend(encode(self.tokenizer, self.texts[self._row(self.current_index)],
                               padding=False, truncation=True, max_length=S1))
             self.current_index += 1
-        # the last document was cut: start the next sample from its beginning again
-        self.current_index -= 1
+            docs += 1
+        # the last document was cut: start the next sample from its beginning again.
+        # (The reference always steps back, so a single document of ≥ S+1 tokens is
+        # repeated forever; stepping back only when the sample packed more than one
+        # document keeps its order otherwise and guarantees progress.)
+        if docs > 1:
+            self.current_index -= 1
         buf = buf[:S1]
         self.token_buffer = buf
         self.samples += 1

@@ -125,14 +125,17 @@ class FlatAdamW(torch.optim.Optimizer):
         return None
 
     # ------------------------------------------------------------------ state dict
-    def state_dict(self):
+    def state_dict(self, exp_avg: Optional[torch.Tensor] = None, exp_avg_sq: Optional[torch.Tensor] = None):
+        """torch AdamW ``state_dict`` structure; moments are views of the flat buffers
+        (or of ``exp_avg``/``exp_avg_sq`` — e.g. their host snapshot — when given)."""
+        M = self.exp_avg if exp_avg is None else exp_avg
+        V = self.exp_avg_sq if exp_avg_sq is None else exp_avg_sq
         state = {}
-        step_t = torch.tensor(float(self.step_count), dtype=torch.float32)
         for i, s in enumerate(self._index_slots):
             state[i] = {
-                "step": step_t.clone(),
-                "exp_avg": self.exp_avg[s.offset : s.offset + s.numel].view(s.shape),
-                "exp_avg_sq": self.exp_avg_sq[s.offset : s.offset + s.numel].view(s.shape),
+                "step": torch.tensor(float(self.step_count), dtype=torch.float32),
+                "exp_avg": M[s.offset : s.offset + s.numel].view(s.shape),
+                "exp_avg_sq": V[s.offset : s.offset + s.numel].view(s.shape),
             }
         groups = []
         idx = 0
@@ -145,15 +148,23 @@ class FlatAdamW(torch.optim.Optimizer):
 
     @torch.no_grad()
     def load_state_dict(self, sd):
+        """Accepts our files and torch AdamW files (per-parameter tensors) alike."""
+        from ..ckpt.state import _flat_source
+
         st = sd["state"]
-        steps = set()
-        for i, s in enumerate(self._index_slots):
-            if i not in st:
+        slots_by_idx = {i: s for i, s in enumerate(self._index_slots)}
+        for key, buf in (("exp_avg", self.exp_avg), ("exp_avg_sq", self.exp_avg_sq)):
+            tensors = {i: st[i][key] for i in slots_by_idx if i in st}
+            src = None
+            if len(tensors) == len(slots_by_idx):
+                src = _flat_source(tensors, slots_by_idx, buf.numel(), buf.dtype)
+            if src is not None:
+                buf.copy_(src, non_blocking=True)
                 continue
-            e = st[i]
-            self.exp_avg[s.offset : s.offset + s.numel].view(s.shape).copy_(e["exp_avg"], non_blocking=True)
-            self.exp_avg_sq[s.offset : s.offset + s.numel].view(s.shape).copy_(e["exp_avg_sq"], non_blocking=True)
-            steps.add(int(float(e["step"])))
+            for i, t in tensors.items():
+                s = slots_by_idx[i]
+                buf[s.offset : s.offset + s.numel].view(s.shape).copy_(t, non_blocking=True)
+        steps = {int(float(st[i]["step"])) for i in slots_by_idx if i in st}
         if steps:
             self.step_count = max(steps)
         for g, sg in zip(self.param_groups, sd["param_groups"]):

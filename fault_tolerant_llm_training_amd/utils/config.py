@@ -127,7 +127,21 @@ def build_parser() -> argparse.ArgumentParser:
     parser.add_argument(
         "--no-async-checkpoint",
         action="store_true",
-        help="Write checkpoints synchronously (torch.save on the main thread)",
+        help="Block the training loop until each periodic checkpoint is durable",
+    )
+    parser.add_argument(
+        "--checkpoint-mode",
+        type=str,
+        default="auto",
+        choices=["auto", "hbm", "host"],
+        help="Snapshot path: hbm = D2D copy into reserved HBM then background D2H; host = D2H "
+        "straight into pinned host memory; auto = hbm when free HBM allows",
+    )
+    parser.add_argument(
+        "--checkpoint-writer-threads", type=int, default=8, help="Parallel pwrite threads of the checkpoint writer"
+    )
+    parser.add_argument(
+        "--prefetch", type=int, default=2, help="Batches prepared ahead by the data-loader thread (0: inline)"
     )
     parser.add_argument(
         "--optimizer-state-dtype",
@@ -155,11 +169,6 @@ def build_parser() -> argparse.ArgumentParser:
         type=str,
         default="",
         help="Job script resubmitted on SIGUSR1 (default: $WORKDIR/train.sh)",
-    )
-    parser.add_argument(
-        "--activation-checkpointing",
-        action="store_true",
-        help="Recompute each block in backward (long sequences)",
     )
     return parser
 

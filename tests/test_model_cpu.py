@@ -1,0 +1,108 @@
+"""Model math vs an independent eager implementation of the reference's model.py.
+
+The reference model (model.py:24-380): RMSNorm in fp32 then ``type_as`` then ×weight,
+complex-multiply RoPE on interleaved pairs, materialised repeat_kv, causal SDPA,
+SwiGLU ``w2(silu(w1 x) * w3 x)``, untied head; loss = CE(sum)/num_items
+(train.py:101-102). Parameters are loaded through the shared state_dict keys.
+"""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from fault_tolerant_llm_training_amd.models.llama import build_model, model_args_for
+
+
+def ref_forward(sd, a, tokens):
+    def rms(x, w):
+        xf = x.float()
+        return (xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + a.norm_eps)).type_as(x) * w
+
+    hd = a.dim // a.n_heads
+    kv = a.kv_heads
+    freqs = 1.0 / (a.rope_theta ** (torch.arange(0, hd, 2)[: hd // 2].float() / hd))
+    cis = torch.polar(torch.ones(a.seq_len, hd // 2), torch.outer(torch.arange(a.seq_len).float(), freqs))
+
+    def rope(x):
+        B, S, H, D = x.shape
+        xc = torch.view_as_complex(x.float().reshape(B, S, H, D // 2, 2))
+        return torch.view_as_real(xc * cis[:S].view(1, S, 1, D // 2)).flatten(3).type_as(x)
+
+    h = sd["tok_embeddings.weight"][tokens]
+    B, S = tokens.shape
+    for i in range(a.n_layers):
+        p = f"layers.{i}."
+        x = rms(h, sd[p + "attention_norm.weight"])
+        q = (x @ sd[p + "attention.wq.weight"].t()).view(B, S, a.n_heads, hd)
+        k = (x @ sd[p + "attention.wk.weight"].t()).view(B, S, kv, hd)
+        v = (x @ sd[p + "attention.wv.weight"].t()).view(B, S, kv, hd)
+        q, k = rope(q), rope(k)
+        rep = a.n_heads // kv
+        k = k[:, :, :, None, :].expand(B, S, kv, rep, hd).reshape(B, S, a.n_heads, hd)
+        v = v[:, :, :, None, :].expand(B, S, kv, rep, hd).reshape(B, S, a.n_heads, hd)
+        o = F.scaled_dot_product_attention(q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2), is_causal=True)
+        o = o.transpose(1, 2).reshape(B, S, -1)
+        h = h + o @ sd[p + "attention.wo.weight"].t()
+        x = rms(h, sd[p + "ffn_norm.weight"])
+        g = F.silu(x @ sd[p + "feed_forward.w1.weight"].t()) * (x @ sd[p + "feed_forward.w3.weight"].t())
+        h = h + g @ sd[p + "feed_forward.w2.weight"].t()
+    h = rms(h, sd["norm.weight"])
+    return h @ sd["output.weight"].t()
+
+
+def test_state_dict_keys_match_reference_layout():
+    a = model_args_for("tiny", vocab_size=128, seq_len=16)
+    m = build_model(a, "cpu", torch.float32, seed=0)
+    keys = list(m.state_dict().keys())
+    exp = ["tok_embeddings.weight"]
+    for i in range(a.n_layers):
+        p = f"layers.{i}."
+        exp += [p + "attention.wq.weight", p + "attention.wk.weight", p + "attention.wv.weight",
+                p + "attention.wo.weight", p + "feed_forward.w1.weight", p + "feed_forward.w2.weight",
+                p + "feed_forward.w3.weight", p + "attention_norm.weight", p + "ffn_norm.weight"]
+    exp += ["norm.weight", "output.weight"]
+    assert keys == exp
+    assert not any("rope" in k or "freqs" in k for k in keys)  # non-persistent tables
+
+
+def test_llama3_8b_shapes():
+    a = model_args_for("llama3-8b", vocab_size=131072, seq_len=2048)
+    assert a.ffn_hidden == 14336  # reference model.py:243-247 rule
+    assert a.head_dim == 128 and a.kv_heads == 8
+    per_layer = 4096 * 4096 * 2 + 2 * 4096 * 1024 + 3 * 4096 * 14336 + 2 * 4096
+    total = 32 * per_layer + 2 * 131072 * 4096 + 4096
+    assert abs(total / 1e9 - 8.053) < 0.001  # 8.05 B
+
+
+@pytest.mark.parametrize("preset", ["tiny"])
+def test_forward_backward_matches_reference_math(preset):
+    torch.manual_seed(0)
+    a = model_args_for(preset, vocab_size=257, seq_len=24)
+    m = build_model(a, "cpu", torch.float32, seed=3)
+    tok = torch.randint(0, 257, (2, 24))
+    lab = torch.randint(0, 257, (2, 24))
+    lab[0, :3] = -100
+    sd = {k: v.detach().clone().requires_grad_(True) for k, v in m.state_dict().items()}
+    logits_ref = ref_forward(sd, a, tok)
+    n = (lab != -100).sum()
+    loss_ref = F.cross_entropy(logits_ref.flatten(0, 1).float(), lab.flatten(), reduction="sum") / n
+    loss_ref.backward()
+    logits = m(tok)
+    assert torch.allclose(logits, logits_ref, atol=1e-4, rtol=1e-4)
+    loss = m(tok, lab)
+    assert math.isclose(loss.item(), loss_ref.item(), rel_tol=1e-5)
+    loss.backward()
+    named = dict(m.named_parameters())
+    for k, v in sd.items():
+        assert torch.allclose(named[k].grad, v.grad, atol=1e-5, rtol=1e-4), k
+
+
+def test_layernorm_variant():
+    a = model_args_for("tiny", vocab_size=64, seq_len=8, norm_type="layernorm")
+    m = build_model(a, "cpu", torch.float32, seed=1)
+    tok = torch.randint(0, 64, (1, 8))
+    loss = m(tok, tok)
+    loss.backward()
+    assert torch.isfinite(loss)
+    assert m.flat.grads.abs().sum() > 0
