@@ -1,0 +1,152 @@
+"""Data parallelism on the CPU with gloo (world_size 2): the RCCL code path's semantics.
+
+* FlatDDP (bucketed all-reduce launched from backward, SUM of globally
+  normalised losses) reproduces the single-process gradient of the global batch;
+* ``train.py`` under torchrun: a SIGUSR1 delivered to ONE rank stops every
+  rank at the same step (MAX vote), rank 0 writes the checkpoint, and the
+  DP resume is bit-identical to an uninterrupted DP run.
+"""
+import os
+import re
+import signal
+import socket
+import subprocess
+import sys
+import time
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from helpers import ROOT, TINY, env_for, kill_group, wait_for_log, write_fake_sbatch
+
+pytestmark = pytest.mark.slow
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, out_dir, bucket_mb):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from fault_tolerant_llm_training_amd.data.synthetic import SyntheticTokens
+    from fault_tolerant_llm_training_amd.models.llama import build_model, model_args_for
+    from fault_tolerant_llm_training_amd.parallel.ddp import FlatDDP
+
+    a = model_args_for("tiny", vocab_size=128, seq_len=16)
+    m = build_model(a, "cpu", torch.float32, seed=5)
+    ddp = FlatDDP(m.flat, m.sinks_in_backward_order(), bucket_mb=bucket_mb)
+    ddp.broadcast_params()
+    ds = SyntheticTokens(128, 16, seed=9, rank=rank, world_size=world, pin=False)
+    for step in range(2):
+        x, y = ds.batch(step, 2)
+        y[0, :3] = -100  # uneven loss-token counts across ranks
+        n = torch.tensor([float((y != -100).sum())])
+        dist.all_reduce(n)
+        loss = m(x, y, 1.0 / n)
+        loss.backward()
+        ddp.finish()
+    torch.save(m.flat.grads.clone(), os.path.join(out_dir, f"g{rank}.pt"))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("bucket_mb", [0.05, 256.0])
+def test_ddp_grads_equal_single_process_global_batch(tmp_path, bucket_mb):
+    world = 2
+    mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path), bucket_mb), nprocs=world,
+                       start_method="spawn")
+    g0 = torch.load(tmp_path / "g0.pt")
+    g1 = torch.load(tmp_path / "g1.pt")
+    assert torch.equal(g0, g1)
+    from fault_tolerant_llm_training_amd.data.synthetic import SyntheticTokens
+    from fault_tolerant_llm_training_amd.models.llama import build_model, model_args_for
+
+    a = model_args_for("tiny", vocab_size=128, seq_len=16)
+    m = build_model(a, "cpu", torch.float32, seed=5)
+    ds = SyntheticTokens(128, 16, seed=9, pin=False)
+    x, y = ds.batch(1, 4)  # global batch of the last step
+    y[0, :3] = -100
+    y[2, :3] = -100
+    loss = m(x, y)
+    loss.backward()
+    assert torch.allclose(g0, m.flat.grads, atol=2e-6, rtol=1e-4)
+
+
+def _torchrun(d, job, args, world=2):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "train.py")] + args
+    env = env_for(d, job, {"OMP_NUM_THREADS": "1"})
+    return cmd, env
+
+
+def _run(d, job, args):
+    cmd, env = _torchrun(d, job, args)
+    r = subprocess.run(cmd, cwd=d, env=env, capture_output=True, text=True, timeout=600)
+    return r.returncode, r.stdout + r.stderr
+
+
+def _rank_pids(parent_pid):
+    import psutil
+
+    kids = psutil.Process(parent_pid).children(recursive=True)
+    out = {}
+    for k in kids:
+        try:
+            env = k.environ()
+        except Exception:
+            continue
+        if "RANK" in env and "train.py" in " ".join(k.cmdline()):
+            out[int(env["RANK"])] = k.pid
+    return out
+
+
+def test_dp_signal_to_one_rank_stops_all_and_resume_is_exact(tmp_path):
+    d = str(tmp_path)
+    write_fake_sbatch(d)
+    ck = ["--checkpoint-path", os.path.join(d, "ck")]
+    base = TINY + ["--synthetic-data", "--vocab-size", "256", "--training-steps", "31", "--lr-warmup-steps", "3"] + ck
+    end = ["--raise-error", "--error-step", "30"]
+    rc, out = _run(d, "100", base + end)
+    assert rc == 0 and "Checkpoint saved at step 30" in out, out
+    assert "Data parallel over 2 ranks" in out
+
+    cmd, env = _torchrun(d, "200", base + end)
+    log = open(os.path.join(d, "dp.log"), "w")
+    p = subprocess.Popen(cmd, cwd=d, env=env, stdout=log, stderr=subprocess.STDOUT, start_new_session=True)
+    try:
+        assert wait_for_log(log.name, "Training step: 5 |", timeout=180), open(log.name).read()
+        pids = {}
+        for _ in range(100):
+            pids = _rank_pids(p.pid)
+            if len(pids) == 2:
+                break
+            time.sleep(0.1)
+        assert set(pids) == {0, 1}
+        os.kill(pids[1], signal.SIGUSR1)  # only rank 1 sees the signal
+        assert p.wait(timeout=180) == 0
+    finally:
+        kill_group(p)
+    out = open(log.name).read()
+    m = re.search(r"Checkpoint saved at step (\d+)", out)
+    assert m and "Job timed out" in out, out
+    c = torch.load(os.path.join(d, "ck", "checkpoint_200.ckpt"), map_location="cpu", weights_only=True)
+    assert c["training_step"] == int(m.group(1))
+    assert isinstance(c["data_loader"], list) and len(c["data_loader"]) == 2
+    assert all(s["next_step"] == c["training_step"] for s in c["data_loader"])
+    assert c["meta"]["world_size"] == 2
+
+    rc, out = _run(d, "300", base + end + ["--checkpoint-id", "200"])
+    assert rc == 0 and f"Resuming training from training_step {c['training_step']}" in out, out
+    a = torch.load(os.path.join(d, "ck", "checkpoint_100.ckpt"), map_location="cpu", weights_only=True)
+    b = torch.load(os.path.join(d, "ck", "checkpoint_300.ckpt"), map_location="cpu", weights_only=True)
+    for k in a["model"]:
+        assert torch.equal(a["model"][k], b["model"][k]), k
+    for i in a["optimizer"]["state"]:
+        assert torch.equal(a["optimizer"]["state"][i]["exp_avg_sq"], b["optimizer"]["state"][i]["exp_avg_sq"])
