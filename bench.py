@@ -41,13 +41,15 @@ def parse():
     ap.add_argument("--bucket-mb", type=float, default=256.0)
     ap.add_argument("--ckpt-dir", default="", help="also time one async checkpoint save into this dir")
     ap.add_argument("--device", default="cuda")
+    ap.add_argument("--dp-mode", default="", choices=["", "allreduce", "zero1"])
+    ap.add_argument("--no-overlap", action="store_true", help="optimizer as a serial phase (A/B)")
     return ap.parse_args()
 
 
 def main():
     a = parse()
     from fault_tolerant_llm_training_amd.parallel import dist as fdist
-    from fault_tolerant_llm_training_amd.parallel.ddp import FlatDDP
+    from fault_tolerant_llm_training_amd.parallel.ddp import GradReducer
     from fault_tolerant_llm_training_amd.models.llama import build_model, model_args_for, flops_per_token
     from fault_tolerant_llm_training_amd.optim.adamw import FlatAdamW
     from fault_tolerant_llm_training_amd.utils.lr import build_lr_scheduler
@@ -61,10 +63,12 @@ def main():
 
     margs = model_args_for(a.model, vocab_size=a.vocab_size, seq_len=a.seq_len)
     model = build_model(margs, dev, torch.bfloat16, seed=1234)
-    opt = FlatAdamW(model.parameters(), model.flat, lr=5e-5, max_grad_norm=1.0)
+    red = GradReducer(model.flat, model.sinks_in_backward_order(), bucket_mb=a.bucket_mb,
+                      mode=a.dp_mode or None, overlap=not a.no_overlap)
+    opt = FlatAdamW(model.parameters(), model.flat, lr=5e-5, max_grad_norm=1.0, reducer=red)
+    model.gate = opt.gate
     sched = build_lr_scheduler(opt, 100)
-    ddp = FlatDDP(model.flat, model.sinks_in_backward_order(), bucket_mb=a.bucket_mb)
-    ddp.broadcast_params()
+    red.broadcast_params()
 
     data = SyntheticTokens(a.vocab_size, a.seq_len, seed=4321, rank=info.rank, world_size=world)
     B, S = a.batch_size, a.seq_len
@@ -76,7 +80,7 @@ def main():
         lab = lab.to(dev, non_blocking=True)
         loss = model(tok, lab, inv_count)
         loss.backward()
-        ddp.finish()
+        red.finish()
         opt.clip_grad_norm_(1.0)
         opt.step()
         sched.step()
@@ -90,6 +94,7 @@ def main():
     t0 = time.perf_counter()
     for i in range(a.steps):
         loss = step(a.warmup + i)
+    opt.gate.wait_all()
     torch.cuda.synchronize()
     fdist.barrier()
     torch.cuda.synchronize()
@@ -121,8 +126,10 @@ def main():
         "mfu_vs_2.5PF_dense": round(mfu, 4),
         "final_loss": round(final_loss, 4),
         "params": model.num_params(),
+        "grad_mode": red.mode,
+        "buckets": len(red.buckets),
     }
-    if a.ckpt_dir:
+    if a.ckpt_dir and not opt.zero1:
         from fault_tolerant_llm_training_amd.ckpt.bench_save import time_checkpoint_save
 
         out["ckpt_save"] = time_checkpoint_save(model, opt, sched, a.ckpt_dir, info)

@@ -168,7 +168,44 @@ void adamw_(const at::Tensor& p, const at::Tensor& g, const at::Tensor& m, const
   FT_LAUNCH_CHECK();
 }
 
+// Per-bucket partial sums of squares, launched while backward is still running:
+// block i of the launch writes partial[i] (grid = partial.numel()), so the total is
+// a fixed-order sum independent of when each bucket finished (deterministic).
+void sumsq_into_(const at::Tensor& grad, const at::Tensor& partial) {
+  FT_CHECK_CUDA(grad);
+  FT_CHECK_CONTIG(grad);
+  FT_CHECK_F32(partial);
+  FT_CHECK_CONTIG(partial);
+  TORCH_CHECK(grad.numel() % 8 == 0, "sumsq_into: numel must be a multiple of 8");
+  TORCH_CHECK(partial.numel() >= 1 && partial.numel() <= 65535, "sumsq_into: bad partial size");
+  const at::DeviceGuard guard(grad.device());
+  const long n8 = grad.numel() / 8;
+  const int nb = (int)partial.numel();
+  if (grad.scalar_type() == at::kBFloat16)
+    hipLaunchKernelGGL(sumsq_kernel<bf16_t>, dim3(nb), dim3(256), 0, ft_stream(), cptr<bf16_t>(grad),
+                       n8, mptr<float>(partial));
+  else if (grad.scalar_type() == at::kFloat)
+    hipLaunchKernelGGL(sumsq_kernel<float>, dim3(nb), dim3(256), 0, ft_stream(), cptr<float>(grad),
+                       n8, mptr<float>(partial));
+  else
+    TORCH_CHECK(false, "sumsq_into: unsupported dtype");
+  FT_LAUNCH_CHECK();
+}
+
+// stats = [norm, clip coef, nonfinite] from a vector of partial sums of squares.
+void norm_finish_(const at::Tensor& partial, const at::Tensor& stats, double max_norm) {
+  FT_CHECK_CUDA(partial);
+  FT_CHECK_F32(partial);
+  FT_CHECK_F32(stats);
+  const at::DeviceGuard guard(partial.device());
+  hipLaunchKernelGGL(norm_finish_kernel, dim3(1), dim3(256), 0, ft_stream(), cptr<float>(partial),
+                     (int)partial.numel(), 1.f, (float)max_norm, mptr<float>(stats));
+  FT_LAUNCH_CHECK();
+}
+
 TORCH_LIBRARY_FRAGMENT(ftamd, m) {
+  m.def("sumsq_into_(Tensor grad, Tensor(a!) partial) -> ()", &sumsq_into_);
+  m.def("norm_finish_(Tensor partial, Tensor(a!) stats, float max_norm) -> ()", &norm_finish_);
   m.def("grad_norm_(Tensor grad, Tensor(a!) stats, float max_norm) -> ()", &grad_norm_);
   m.def(
       "adamw_(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, Tensor stats, float lr, float "

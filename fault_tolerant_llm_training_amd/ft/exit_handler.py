@@ -82,7 +82,9 @@ def handle_exit(save_checkpoint: Callable[[], object], training_step: int, exit_
     else:
         logger.info(f"[EXIT HANDLER] Unknown exit signal {exit_type}, terminating.")
         return
-    save_checkpoint()
+    if save_checkpoint() is False:
+        logger.error(f"[EXIT HANDLER] Checkpoint could not be saved at step {training_step}")
+        return
     logger.info(f"[EXIT HANDLER] Checkpoint saved at step {training_step}")
     if exit_type == SIGUSR1 and is_main:
         script = sbatch_script or os.path.join(os.getenv("WORKDIR", ""), "train.sh")

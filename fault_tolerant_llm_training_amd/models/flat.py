@@ -52,11 +52,15 @@ class FlatParamSpace:
             n = p.numel()
             self.slots[name] = Slot(name, tuple(p.shape), off, n)
             off += (n + ALIGN - 1) // ALIGN * ALIGN
-        self.numel = (off + 7) // 8 * 8
+        # a multiple of ALIGN: every bucket cut at slot boundaries splits evenly into
+        # 8-element-aligned ZeRO shards for up to 8 ranks
+        self.numel = (off + ALIGN - 1) // ALIGN * ALIGN
+        self.align = ALIGN
         self.params = torch.zeros(self.numel, dtype=dtype, device=self.device)
         # zero-initialised once: alignment gaps stay zero forever (no NaN in the norm)
         self.grads = torch.zeros(self.numel, dtype=dtype, device=self.device)
         self.layout = list(layout)
+        self.model_ref = None
         self.sinks: Dict[str, GradSink] = {}
         self.param_objs: Dict[str, nn.Parameter] = {}
         modules = dict(model.named_modules())

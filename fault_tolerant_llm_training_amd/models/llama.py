@@ -158,6 +158,8 @@ class Transformer(nn.Module):
         self.norm = _Weight(a.dim)
         self.output = _Weight(a.vocab_size, a.dim)
         self.flat: Optional[FlatParamSpace] = None
+        self.gate = None  # optim.adamw.ParamGate: per-layer wait for the optimizer's updates
+        self._ranges = None
 
     # ------------------------------------------------------------------ materialisation
     def flat_layout(self):
@@ -187,8 +189,27 @@ class Transformer(nn.Module):
                 [f"layers.{i}.attention.wq.weight", f"layers.{i}.attention.wk.weight", f"layers.{i}.attention.wv.weight"])
             ff.w13, ff.w13_sink = self.flat.fused(
                 [f"layers.{i}.feed_forward.w1.weight", f"layers.{i}.feed_forward.w3.weight"])
+        self._ranges = self._param_ranges()
         self.init_weights(seed)
         return self
+
+    def _param_ranges(self):
+        """Flat [lo, hi) of the weights used by: embedding, each layer, final norm + head."""
+        sl = self.flat.slots
+
+        def span(prefix):
+            ss = [s for n, s in sl.items() if n.startswith(prefix)]
+            return min(s.offset for s in ss), max(s.offset + s.numel for s in ss)
+
+        emb = span("tok_embeddings.")
+        layers = [span(f"layers.{i}.") for i in range(self.n_layers)]
+        lo_n, hi_n = span("norm.")
+        lo_o, hi_o = span("output.")
+        return emb, layers, (min(lo_n, lo_o), max(hi_n, hi_o))
+
+    def _wait(self, rng):
+        if self.gate is not None:
+            self.gate.wait(*rng)
 
     @torch.no_grad()
     def init_weights(self, seed: int = 1234):
@@ -219,10 +240,14 @@ class Transformer(nn.Module):
         (sum of token NLL × inv_count, reference train.py:101-102); else logits."""
         B, S = tokens.shape
         sk = lambda p: getattr(p, "_ft_sink", None)  # noqa: E731
+        emb_r, layer_r, final_r = self._ranges
+        self._wait(emb_r)
         h = Fx.embedding(tokens, self.tok_embeddings.weight, sk(self.tok_embeddings.weight))
         cos, sin = self.rope_cos, self.rope_sin
-        for layer in self.layers.values():
+        for i, layer in enumerate(self.layers.values()):
+            self._wait(layer_r[i])
             h = layer(h, cos, sin, S)
+        self._wait(final_r)
         a = self.model_args
         h = Fx.norm(h, self.norm.weight, sk(self.norm.weight), a.norm_eps, a.norm_type == "layernorm")
         if labels is None:

@@ -1,4 +1,4 @@
-"""Flat-buffer AdamW with on-device gradient clipping.
+"""Flat-buffer AdamW with on-device gradient clipping, pipelined into the next step.
 
 Replaces the reference's ``torch.optim.AdamW(model.parameters(), lr,
 fused=args.fused_optimizer)`` (train.py:68) plus ``clip_grad_norm_``
@@ -9,19 +9,29 @@ eps 1e-8, weight_decay 0.01). It subclasses ``torch.optim.Optimizer`` so
 ``exp_avg``, ``exp_avg_sq`` + ``param_groups``) so checkpoints interoperate
 with the reference layout.
 
-On the GPU a step is: one multi-block sum-of-squares over the flat gradient
-buffer, one finishing block that computes the norm and clip coefficient into a
-device tensor, and one streaming AdamW kernel over the flat parameter /
-gradient / moment buffers that reads the coefficient from HBM — no host sync.
-A non-finite norm makes the kernel skip the update; :meth:`check_finite`
-reports it one step later (deferred, so the host never stalls the GPU).
+GPU step (with a :class:`~..parallel.ddp.GradReducer`):
+
+1. the reducer already summed squares of every gradient bucket on a side
+   stream while backward was running (after its all-reduce / reduce-scatter);
+2. ``step()`` enqueues on that side stream: the norm + clip coefficient
+   (one block; ZeRO-1 adds a 4-byte all-reduce), then one AdamW launch per
+   bucket **in forward order** (embedding first), each followed by an event
+   (or, under ZeRO-1, the bucket's parameter all-gather);
+3. the next forward waits, layer by layer, only for the buckets holding that
+   layer's weights (:class:`ParamGate`), so the bandwidth-bound optimizer pass
+   overlaps the compute-bound GEMMs of the next step instead of running as a
+   serial phase.
+
+A non-finite norm makes every update kernel skip (no host sync);
+:meth:`check_finite` reports it one step later.
 """
 from __future__ import annotations
 
 import math
-from typing import Optional
+from typing import List, Optional, Tuple
 
 import torch
+import torch.distributed as dist
 
 from .._native import kernels
 from ..models.flat import FlatParamSpace
@@ -31,71 +41,147 @@ class NonFiniteGradError(RuntimeError):
     pass
 
 
+class ParamGate:
+    """Per-range readiness of the parameter buffer for the next forward.
+
+    Entries are (lo, hi, handle) with handle a ``torch.cuda.Event`` (recorded on
+    the optimizer stream) or a collective work object (all-gather). The model
+    calls :meth:`wait` with the flat range of the weights it is about to use;
+    the *compute stream* is made to wait — the host never blocks.
+    """
+
+    def __init__(self):
+        self.entries: List[list] = []
+
+    def add(self, lo: int, hi: int, handle) -> None:
+        self.entries.append([lo, hi, handle])
+
+    def wait(self, lo: int, hi: int) -> None:
+        if not self.entries:
+            return
+        cur = None
+        for e in self.entries:
+            h = e[2]
+            if h is None or e[1] <= lo or e[0] >= hi:
+                continue
+            if isinstance(h, torch.cuda.Event):
+                if cur is None:
+                    cur = torch.cuda.current_stream()
+                cur.wait_event(h)
+            else:
+                h.wait()
+            e[2] = None
+        self.entries = [e for e in self.entries if e[2] is not None]
+
+    def wait_all(self) -> None:
+        if self.entries:
+            self.wait(0, 1 << 62)
+
+
 class FlatAdamW(torch.optim.Optimizer):
     def __init__(self, params, flat: FlatParamSpace, lr: float = 1e-3, betas=(0.9, 0.999),
                  eps: float = 1e-8, weight_decay: float = 1e-2, state_dtype: Optional[torch.dtype] = None,
-                 max_grad_norm: float = 0.0, fused: bool = True):
+                 max_grad_norm: float = 0.0, fused: bool = True, reducer=None):
         params = list(params)
         defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, amsgrad=False,
                         maximize=False, foreach=None, capturable=False, differentiable=False,
                         fused=fused, decoupled_weight_decay=True)
         super().__init__(params, defaults)
         self.flat = flat
+        self.reducer = reducer
+        self.zero1 = reducer is not None and reducer.mode == "zero1"
         sd = state_dtype or flat.dtype
-        self.exp_avg = torch.zeros(flat.numel, dtype=sd, device=flat.device)
-        self.exp_avg_sq = torch.zeros(flat.numel, dtype=sd, device=flat.device)
+        n = reducer.shard_numel if self.zero1 else flat.numel
+        self.exp_avg = torch.zeros(n, dtype=sd, device=flat.device)
+        self.exp_avg_sq = torch.zeros(n, dtype=sd, device=flat.device)
         self.step_count = 0
         self.max_grad_norm = float(max_grad_norm)
         self.stats = torch.zeros(3, dtype=torch.float32, device=flat.device)  # norm, coef, nonfinite
         self._host_stats = torch.zeros(3, dtype=torch.float32, pin_memory=flat.device.type == "cuda")
         self._stats_event = None
         self._stats_step = -1
+        self.gate = ParamGate()
         # parameter index (reference order) -> flat slot
         name_of = {id(p): n for n, p in flat.param_objs.items()}
         self._index_slots = [flat.slots[name_of[id(p)]] for p in params]
 
     # ------------------------------------------------------------------ step
-    @torch.no_grad()
     def clip_grad_norm_(self, max_norm: Optional[float] = None) -> torch.Tensor:
-        """Compute ||g|| and the clip coefficient on device; returns the norm (device scalar)."""
-        mn = self.max_grad_norm if max_norm is None else float(max_norm)
-        self.max_grad_norm = mn
-        g = self.flat.grads
-        if g.is_cuda:
-            kernels().grad_norm_(g, self.stats, mn)
-        else:
-            norm = torch.linalg.vector_norm(g.float())
-            bad = not torch.isfinite(norm)
-            coef = 1.0 if (mn <= 0 or bad) else min(1.0, mn / (float(norm) + 1e-6))
-            self.stats.copy_(torch.tensor([float(norm), coef, 1.0 if bad else 0.0]))
-        self._clipped = True
+        """Set the clipping threshold; the norm itself is computed on device by :meth:`step`
+        (``stats[0]`` holds it afterwards). Clipping is real."""
+        if max_norm is not None:
+            self.max_grad_norm = float(max_norm)
         return self.stats[0]
+
+    def _stream_ctx(self):
+        r = self.reducer
+        if r is not None and r.overlap:
+            return torch.cuda.stream(r.side)
+        import contextlib
+
+        return contextlib.nullcontext()
+
+    def _hyper(self):
+        grp = self.param_groups[0]
+        b1, b2 = grp["betas"]
+        return float(grp["lr"]), b1, b2, grp["eps"], grp["weight_decay"]
+
+    def _update(self, p, g, m, v, lr, b1, b2, eps, wd):
+        if p.is_cuda:
+            kernels().adamw_(p, g, m, v, self.stats, lr, b1, b2, eps, wd, self.step_count)
+        else:
+            _adamw_reference(p, g, m, v, self.stats, lr, b1, b2, eps, wd, self.step_count)
 
     @torch.no_grad()
     def step(self, closure=None):
-        if not getattr(self, "_clipped", False):
-            self.clip_grad_norm_()
-        self._clipped = False
         self.step_count += 1
-        grp = self.param_groups[0]
-        lr = float(grp["lr"])
-        b1, b2 = grp["betas"]
-        eps, wd = grp["eps"], grp["weight_decay"]
+        lr, b1, b2, eps, wd = self._hyper()
         f = self.flat
-        if f.params.is_cuda:
-            kernels().adamw_(f.params, f.grads, self.exp_avg, self.exp_avg_sq, self.stats, lr, b1, b2,
-                             eps, wd, self.step_count)
+        r = self.reducer
+        cuda = f.params.is_cuda
+        if r is None:
+            # stand-alone: whole-buffer norm + one AdamW launch on the current stream
+            if cuda:
+                kernels().grad_norm_(f.grads, self.stats, self.max_grad_norm)
+            else:
+                _norm_reference(f.grads.float().pow(2).sum().reshape(1), self.stats, self.max_grad_norm)
+            self._update(f.params, f.grads, self.exp_avg, self.exp_avg_sq, lr, b1, b2, eps, wd)
+            self._publish_stats()
+            return None
+        if r.overlap:
+            r.side.wait_stream(torch.cuda.current_stream())
+        with self._stream_ctx():
+            total = r.global_sumsq()
+            if cuda:
+                kernels().norm_finish_(total, self.stats, self.max_grad_norm)
+            else:
+                _norm_reference(total.sum().reshape(1), self.stats, self.max_grad_norm)
+            self._publish_stats()
+            for b in sorted(r.buckets, key=lambda b: b.lo):  # forward order
+                slo, shi = r.state_range(b)
+                self._update(r.param_for_update(b), r.grad_for_update(b), self.exp_avg[slo:shi],
+                             self.exp_avg_sq[slo:shi], lr, b1, b2, eps, wd)
+                if self.zero1:
+                    work = dist.all_gather_into_tensor(f.params[b.lo : b.hi], r.param_shard(b),
+                                                       group=r.group, async_op=True)
+                    if r.overlap:
+                        self.gate.add(b.lo, b.hi, work)
+                    else:
+                        work.wait()
+                elif r.overlap:
+                    b.event.record()
+                    self.gate.add(b.lo, b.hi, b.event)
+        return None
+
+    def _publish_stats(self):
+        if self.stats.is_cuda:
             self._host_stats.copy_(self.stats, non_blocking=True)
             if self._stats_event is None:
                 self._stats_event = torch.cuda.Event()
             self._stats_event.record()
-            self._stats_step = self.step_count
         else:
-            _adamw_reference(f.params, f.grads, self.exp_avg, self.exp_avg_sq, self.stats, lr, b1, b2,
-                             eps, wd, self.step_count)
             self._host_stats.copy_(self.stats)
-            self._stats_step = self.step_count
-        return None
+        self._stats_step = self.step_count
 
     def check_finite(self, block: bool = False) -> Optional[float]:
         """Deferred non-finite check of the last step's gradient norm.
@@ -124,10 +210,28 @@ class FlatAdamW(torch.optim.Optimizer):
         """No-op: every backward overwrites the flat gradient buffer (beta=0 writes)."""
         return None
 
+    # ------------------------------------------------------------------ full-layout state
+    def shard_pieces(self) -> List[Tuple[int, int, int]]:
+        """ZeRO-1: (flat_lo, state_lo, length) pieces of the full moment layout owned here."""
+        r = self.reducer
+        return [(b.lo + r.rank * b.shard_len, b.shard_lo, b.shard_len) for b in r.buckets]
+
+    @torch.no_grad()
+    def gather_full_state(self, out_m: torch.Tensor, out_v: torch.Tensor) -> None:
+        """ZeRO-1: assemble the full-layout moments (flat parameter layout) on every rank."""
+        r = self.reducer
+        for b in r.buckets:
+            slo, shi = r.state_range(b)
+            dist.all_gather_into_tensor(out_m[b.lo : b.hi], self.exp_avg[slo:shi], group=r.group)
+            dist.all_gather_into_tensor(out_v[b.lo : b.hi], self.exp_avg_sq[slo:shi], group=r.group)
+
     # ------------------------------------------------------------------ state dict
     def state_dict(self, exp_avg: Optional[torch.Tensor] = None, exp_avg_sq: Optional[torch.Tensor] = None):
-        """torch AdamW ``state_dict`` structure; moments are views of the flat buffers
-        (or of ``exp_avg``/``exp_avg_sq`` — e.g. their host snapshot — when given)."""
+        """torch AdamW ``state_dict`` structure; moments are views of full-layout buffers
+        (``exp_avg``/``exp_avg_sq`` when given — e.g. their host snapshot — else our own;
+        under ZeRO-1 the full layout must be given, see :meth:`gather_full_state`)."""
+        if self.zero1 and exp_avg is None:
+            raise RuntimeError("ZeRO-1 optimizer state is sharded: pass full-layout moments")
         M = self.exp_avg if exp_avg is None else exp_avg
         V = self.exp_avg_sq if exp_avg_sq is None else exp_avg_sq
         state = {}
@@ -153,17 +257,23 @@ class FlatAdamW(torch.optim.Optimizer):
 
         st = sd["state"]
         slots_by_idx = {i: s for i, s in enumerate(self._index_slots)}
+        numel = self.flat.numel
         for key, buf in (("exp_avg", self.exp_avg), ("exp_avg_sq", self.exp_avg_sq)):
             tensors = {i: st[i][key] for i in slots_by_idx if i in st}
             src = None
             if len(tensors) == len(slots_by_idx):
-                src = _flat_source(tensors, slots_by_idx, buf.numel(), buf.dtype)
-            if src is not None:
+                src = _flat_source(tensors, slots_by_idx, numel, buf.dtype)
+            if src is None:
+                # per-tensor file: assemble the full layout on the host first
+                src = torch.zeros(numel, dtype=buf.dtype)
+                for i, t in tensors.items():
+                    s = slots_by_idx[i]
+                    src[s.offset : s.offset + s.numel].view(s.shape).copy_(t)
+            if self.zero1:
+                for flo, slo, n in self.shard_pieces():
+                    buf[slo : slo + n].copy_(src[flo : flo + n], non_blocking=True)
+            else:
                 buf.copy_(src, non_blocking=True)
-                continue
-            for i, t in tensors.items():
-                s = slots_by_idx[i]
-                buf[s.offset : s.offset + s.numel].view(s.shape).copy_(t, non_blocking=True)
         steps = {int(float(st[i]["step"])) for i in slots_by_idx if i in st}
         if steps:
             self.step_count = max(steps)
@@ -174,6 +284,13 @@ class FlatAdamW(torch.optim.Optimizer):
 
     def moments(self):
         return self.exp_avg, self.exp_avg_sq
+
+
+def _norm_reference(sumsq: torch.Tensor, stats: torch.Tensor, max_norm: float) -> None:
+    norm = float(sumsq.sqrt())
+    bad = not math.isfinite(norm)
+    coef = 1.0 if (max_norm <= 0 or bad) else min(1.0, max_norm / (norm + 1e-6))
+    stats.copy_(torch.tensor([norm, coef, 1.0 if bad else 0.0]))
 
 
 def _adamw_reference(p, g, m, v, stats, lr, b1, b2, eps, wd, step):

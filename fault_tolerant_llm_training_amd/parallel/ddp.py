@@ -1,23 +1,37 @@
-"""Data parallelism over the flat gradient buffer (RCCL over xGMI).
+"""Gradient pipeline: buckets, collectives over RCCL/xGMI, overlapped grad-norm.
 
-Buckets are contiguous ranges of the flat gradient buffer, cut at parameter
-boundaries in *reverse* layout order (the order backward produces them: LM
-head first, embedding last). Backward kernels write each weight gradient
-straight into its slice and call :meth:`GradSink.ready`; when every element of
-a bucket has been written, its ``all_reduce(SUM)`` is launched asynchronously
-on RCCL's stream while the compute stream keeps running backward — the
-all-reduce of layer ``l`` overlaps the backward of layers ``< l``.
-:meth:`finish` makes the compute stream wait for the outstanding collectives
-(stream-ordered; the host is never blocked).
+Every weight gradient is written straight into the flat gradient buffer by its
+backward kernel/GEMM, which then calls :meth:`GradSink.ready`. Buckets are
+contiguous ranges of that buffer cut at parameter boundaries in *reverse*
+layout order (the order backward produces them: LM head first, embedding
+last). The moment the last gradient of a bucket has been enqueued, the bucket's
+work is launched while the compute stream keeps running backward:
 
-The loss is normalised by the *global* token count (see trainer), so SUM (not
-AVG) reproduces the single-process gradient of the global batch exactly.
+``local``     (1 rank)  side stream: partial sum of squares of the bucket.
+``allreduce`` (DP)      RCCL ``all_reduce(SUM)`` of the bucket, then its
+                        partial sum of squares on the side stream.
+``zero1``     (DP)      RCCL ``reduce_scatter`` of the bucket into this rank's
+                        1/W shard (ZeRO-1: optimizer state is sharded), then the
+                        shard's partial sum of squares. After AdamW updates the
+                        shard, an ``all_gather`` republishes the bucket's
+                        parameters (``optim.adamw``).
 
-Bucket size: on an 8× MI355X node every GPU has 7 xGMI links (~153 GB/s each);
-a ring all-reduce per channel is per-link bound, and RCCL spreads channels
-over links only for messages large enough to fill them. Default 256 MiB
-buckets (Llama-3-8B: 16 GB of bf16 gradients → ~64 collectives/step) keep
-launches few while still exposing ~30 overlap points across backward.
+So the gradient norm needed for clipping (reference utils.py:58-63) is
+finished a few µs after backward ends, and the optimizer (which the
+reference runs as a separate serial phase, train.py:107-109) starts at once.
+
+The loss is normalised by the *global* token count (trainer), so SUM (not
+AVG) reproduces the single-process gradient of the global batch.
+
+Bucket size: on an 8× MI355X node every GPU has 7 xGMI links (~153 GB/s
+each, point to point). A ring collective is per-link bound and RCCL only
+spreads a collective over several channels/links when the message is large,
+so buckets are large (default 256 MiB): Llama-3-8B's 16 GB of bf16 gradients
+become ~64 collectives per step — few launches, still ~2 overlap points per
+transformer layer. ZeRO-1 moves the same bytes as all-reduce (reduce-scatter +
+all-gather) but each rank updates and stores only 1/W of the AdamW state: the
+bandwidth-bound optimizer pass (≈20 ms for 8B params on one GPU) shrinks W×,
+and 288 GB of HBM is not the limit for the replicated parameters anyway.
 """
 from __future__ import annotations
 
@@ -26,53 +40,118 @@ from typing import List, Optional
 import torch
 import torch.distributed as dist
 
+from .._native import kernels
 from ..models.flat import FlatParamSpace
 from ..ops.grad_sink import GradSink
 
+MODES = ("local", "allreduce", "zero1")
+PARTIALS_PER_BUCKET = 128
 
-class _Bucket:
-    __slots__ = ("lo", "hi", "needed", "filled", "launched")
 
-    def __init__(self, lo, hi, needed):
-        self.lo, self.hi, self.needed = lo, hi, needed
+class Bucket:
+    __slots__ = ("idx", "lo", "hi", "needed", "filled", "launched", "work", "part_lo", "part_hi",
+                 "shard_lo", "shard_len", "event")
+
+    def __init__(self, idx, lo, hi, needed):
+        self.idx, self.lo, self.hi, self.needed = idx, lo, hi, needed
         self.filled = 0
         self.launched = False
+        self.work = None
+        self.part_lo = self.part_hi = 0
+        self.shard_lo = 0     # offset of this bucket's shard in the rank-local shard buffers
+        self.shard_len = 0    # elements per rank
+        self.event = None
+
+    @property
+    def numel(self):
+        return self.hi - self.lo
 
 
-class FlatDDP:
+def make_buckets(flat: FlatParamSpace, bucket_mb: float) -> List[Bucket]:
+    """Cut the flat buffer into ~bucket_mb ranges at slot boundaries, highest address first."""
+    es = flat.grads.element_size()
+    cap = max(1, int(bucket_mb * (1 << 20) / es))
+    slots = sorted(flat.slots.values(), key=lambda s: s.offset, reverse=True)
+    out: List[Bucket] = []
+    hi = flat.numel
+    needed = 0
+    for s in slots:
+        needed += s.numel
+        if hi - s.offset >= cap:
+            out.append(Bucket(len(out), s.offset, hi, needed))
+            hi, needed = s.offset, 0
+    if needed or hi > 0:
+        out.append(Bucket(len(out), 0, hi, needed))
+    return out
+
+
+class GradReducer:
     def __init__(self, flat: FlatParamSpace, extra_sinks: List[GradSink], bucket_mb: float = 256.0,
-                 group=None):
+                 mode: Optional[str] = None, group=None, overlap: Optional[bool] = None):
         self.flat = flat
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
-        es = flat.grads.element_size()
-        cap = max(1, int(bucket_mb * (1 << 20) / es))
-        slots = sorted(flat.slots.values(), key=lambda s: s.offset, reverse=True)
-        self.buckets: List[_Bucket] = []
-        hi = None
-        lo = None
-        needed = 0
-        for s in slots:
-            if hi is None:
-                hi = flat.numel if not self.buckets else self.buckets[-1].lo
-            lo = s.offset
-            needed += s.numel
-            if (hi - lo) >= cap:
-                self.buckets.append(_Bucket(lo, hi, needed))
-                hi, needed = None, 0
-        if hi is not None:
-            self.buckets.append(_Bucket(0, hi, needed))
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        if mode is None:
+            mode = "local" if self.world == 1 else "zero1"
+        if mode not in MODES:
+            raise ValueError(f"unknown gradient mode {mode!r}")
+        if self.world == 1:
+            mode = "local"
+        if mode == "zero1" and flat.align % (8 * self.world):
+            mode = "allreduce"  # shards must stay 8-element aligned for the vector kernels
+        self.mode = mode
+        self.cuda = flat.device.type == "cuda"
+        self.overlap = self.cuda if overlap is None else (overlap and self.cuda)
+        self.buckets = make_buckets(flat, bucket_mb)
+        # partial sums of squares: a fixed slice per bucket -> deterministic total
+        p = 0
+        for b in self.buckets:
+            n = b.numel // self.world if mode == "zero1" else b.numel
+            k = max(1, min(PARTIALS_PER_BUCKET, (n // 8 + 255) // 256))
+            b.part_lo, b.part_hi = p, p + k
+            p += k
+        self.partials = torch.zeros(p, dtype=torch.float32, device=flat.device)
+        self.sumsq_total = torch.zeros(1, dtype=torch.float32, device=flat.device)
+        # ZeRO-1 shard layout: bucket b's shard for this rank, packed in forward order
+        self.shard_numel = 0
+        if mode == "zero1":
+            for b in sorted(self.buckets, key=lambda b: b.lo):
+                b.shard_len = b.numel // self.world
+                b.shard_lo = self.shard_numel
+                self.shard_numel += b.shard_len
+            self.grad_shard = torch.zeros(self.shard_numel, dtype=flat.dtype, device=flat.device)
         else:
-            self.buckets[-1].lo = 0
-        self._starts = [b.lo for b in self.buckets]  # descending
-        self.works = []
-        self.enabled = self.world > 1
+            self.grad_shard = None
+        self.side = torch.cuda.Stream(device=flat.device) if self.overlap else None
+        if self.cuda:
+            for b in self.buckets:
+                b.event = torch.cuda.Event()
         for sink in list(flat.sinks.values()) + list(extra_sinks):
             sink.hook = self._on_ready
+        self.comm = self.world > 1
 
+    # ---------------------------------------------------------------- shard views
+    def param_shard(self, b: Bucket) -> torch.Tensor:
+        lo = b.lo + self.rank * b.shard_len
+        return self.flat.params[lo : lo + b.shard_len]
+
+    def grad_for_update(self, b: Bucket) -> torch.Tensor:
+        if self.mode == "zero1":
+            return self.grad_shard[b.shard_lo : b.shard_lo + b.shard_len]
+        return self.flat.grads[b.lo : b.hi]
+
+    def param_for_update(self, b: Bucket) -> torch.Tensor:
+        return self.param_shard(b) if self.mode == "zero1" else self.flat.params[b.lo : b.hi]
+
+    def state_range(self, b: Bucket):
+        """(lo, hi) of bucket b in the optimizer-state buffers of this rank."""
+        if self.mode == "zero1":
+            return b.shard_lo, b.shard_lo + b.shard_len
+        return b.lo, b.hi
+
+    # ---------------------------------------------------------------- backward hooks
     def _on_ready(self, sink: GradSink) -> None:
-        if not self.enabled:
-            return
         for b in self.buckets:
             if b.hi <= sink.start:
                 break  # buckets are in descending address order
@@ -82,31 +161,75 @@ class FlatDDP:
                 if b.filled >= b.needed and not b.launched:
                     self._launch(b)
 
-    def _launch(self, b: _Bucket) -> None:
+    def _sumsq(self, g: torch.Tensor, b: Bucket) -> None:
+        part = self.partials[b.part_lo : b.part_hi]
+        if g.is_cuda:
+            kernels().sumsq_into_(g, part)
+        else:
+            part.zero_()
+            part[0] = g.float().pow(2).sum()
+
+    def _launch(self, b: Bucket) -> None:
         b.launched = True
-        view = self.flat.grads[b.lo : b.hi]
-        self.works.append(dist.all_reduce(view, op=dist.ReduceOp.SUM, group=self.group, async_op=True))
+        grads = self.flat.grads[b.lo : b.hi]
+        if self.mode == "allreduce":
+            b.work = dist.all_reduce(grads, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+        elif self.mode == "zero1":
+            out = self.grad_shard[b.shard_lo : b.shard_lo + b.shard_len]
+            b.work = dist.reduce_scatter_tensor(out, grads, op=dist.ReduceOp.SUM, group=self.group,
+                                                async_op=True)
+        if not self.overlap:
+            return  # CPU / no side stream: sums are taken in finish()
+        side = self.side
+        if b.work is None:
+            b.event.record()  # on the compute stream, after the bucket's last gradient kernel
+            side.wait_event(b.event)
+        with torch.cuda.stream(side):
+            if b.work is not None:
+                b.work.wait()  # side stream waits for the collective (host does not)
+                b.work = None
+            self._sumsq(self.grad_for_update(b), b)
 
     def finish(self) -> None:
-        """Launch stragglers, make the current stream wait for every bucket, reset."""
-        if not self.enabled:
-            return
+        """Launch stragglers; after this, ``partials`` hold every bucket's sum of squares
+        (on the side stream when overlapping, else synchronously)."""
         for b in self.buckets:
             if not b.launched:
                 self._launch(b)
-        for w in self.works:
-            w.wait()
-        self.works = []
+        if not self.overlap:
+            for b in self.buckets:
+                if b.work is not None:
+                    b.work.wait()
+                    b.work = None
+                self._sumsq(self.grad_for_update(b), b)
         for b in self.buckets:
             b.filled = 0
             b.launched = False
 
+    def global_sumsq(self) -> torch.Tensor:
+        """Partials reduced across ranks when each rank only holds a shard (ZeRO-1).
+
+        Must run on the stream that owns ``partials`` (side stream when overlapping)."""
+        if self.mode != "zero1":
+            return self.partials
+        if self.cuda:
+            torch.sum(self.partials, dim=0, keepdim=True, out=self.sumsq_total)
+        else:
+            self.sumsq_total.copy_(self.partials.sum().reshape(1))
+        dist.all_reduce(self.sumsq_total, op=dist.ReduceOp.SUM, group=self.group)
+        return self.sumsq_total
+
     @torch.no_grad()
     def broadcast_params(self, src: int = 0) -> None:
-        if self.enabled:
+        if self.comm:
             dist.broadcast(self.flat.params, src=src, group=self.group)
 
     def summary(self) -> str:
         es = self.flat.grads.element_size()
-        sizes = [(b.hi - b.lo) * es / 2**20 for b in self.buckets]
-        return f"{len(self.buckets)} buckets, {min(sizes):.0f}-{max(sizes):.0f} MiB"
+        sizes = [b.numel * es / 2**20 for b in self.buckets]
+        return (f"{self.mode}: {len(self.buckets)} buckets, {min(sizes):.0f}-{max(sizes):.0f} MiB"
+                + (f", shard {self.shard_numel * es / 2**30:.2f} GiB/rank" if self.mode == "zero1" else ""))
+
+
+# Back-compat name used by early scripts.
+FlatDDP = GradReducer

@@ -44,7 +44,7 @@ from .ft.signals import SignalInterrupt, SignalMonitor
 from .models.llama import build_model, flops_per_token, model_args_for
 from .optim.adamw import FlatAdamW
 from .parallel import dist as fdist
-from .parallel.ddp import FlatDDP
+from .parallel.ddp import GradReducer
 from .utils.config import PRECISION_STR_TO_DTYPE, get_args, jobid
 from .utils.logging import init_logger, logger
 from .utils.lr import build_lr_scheduler
@@ -169,8 +169,11 @@ def train(args) -> int:
     model.train()
 
     state_dtype = PRECISION_STR_TO_DTYPE[args.optimizer_state_dtype] if args.optimizer_state_dtype else None
+    reducer = GradReducer(model.flat, model.sinks_in_backward_order(), bucket_mb=args.dp_bucket_mb,
+                          mode=args.dp_mode or None)
     optimizer = FlatAdamW(model.parameters(), model.flat, lr=args.learning_rate, state_dtype=state_dtype,
-                          max_grad_norm=args.grad_max_norm, fused=args.fused_optimizer)
+                          max_grad_norm=args.grad_max_norm, fused=args.fused_optimizer, reducer=reducer)
+    model.gate = optimizer.gate
     if checkpoint is not None:
         optimizer.load_state_dict(checkpoint["optimizer"])
         logger.info("Optimizer loaded from checkpoint")
@@ -191,23 +194,41 @@ def train(args) -> int:
         logger.info("Starting training!")
     del checkpoint
 
-    ddp = FlatDDP(model.flat, model.sinks_in_backward_order(), bucket_mb=args.dp_bucket_mb)
     if info.distributed:
         if training_step == 0:
-            ddp.broadcast_params()
+            reducer.broadcast_params()
         # every rank must agree on where it resumes
         steps = fdist.ctrl_all_gather_object(training_step)
         if len(set(steps)) != 1:
             raise RuntimeError(f"ranks disagree on training_step: {steps}")
-        logger.info(f"Data parallel over {info.world_size} ranks: {ddp.summary()}")
+        logger.info(f"Data parallel over {info.world_size} ranks: {reducer.summary()}")
 
-    engine = CheckpointEngine(
-        {"params": model.flat.params, "exp_avg": optimizer.exp_avg, "exp_avg_sq": optimizer.exp_avg_sq},
-        mode=args.checkpoint_mode, writer_threads=args.checkpoint_writer_threads,
-    )
     ckpt_path = checkpoint_file(args.checkpoint_path, job_id)
+    ckpt = {"engine": None, "full": None}
+
+    def ckpt_engine():
+        if ckpt["engine"] is None:
+            if optimizer.zero1:
+                # ZeRO-1: the moments are sharded; a full-layout copy is assembled in HBM at save time
+                ckpt["full"] = (torch.empty(model.flat.numel, dtype=optimizer.exp_avg.dtype, device=device),
+                                torch.empty(model.flat.numel, dtype=optimizer.exp_avg.dtype, device=device))
+                m, v = ckpt["full"]
+            else:
+                m, v = optimizer.exp_avg, optimizer.exp_avg_sq
+            ckpt["engine"] = CheckpointEngine({"params": model.flat.params, "exp_avg": m, "exp_avg_sq": v},
+                                              mode=args.checkpoint_mode,
+                                              writer_threads=args.checkpoint_writer_threads)
+        return ckpt["engine"]
 
     def save_checkpoint(blocking: bool, collective: bool = True):
+        optimizer.gate.wait_all()  # the snapshot must follow this step's parameter updates
+        if optimizer.zero1 and not collective:
+            logger.error("ZeRO-1 optimizer state is sharded over the ranks; a rank-local error cannot "
+                         "write a complete checkpoint")
+            return False
+        engine = ckpt_engine()
+        if optimizer.zero1:
+            optimizer.gather_full_state(*ckpt["full"])
         if collective:
             states = fdist.ctrl_all_gather_object(loader.state_dict())
         else:  # rank-local save (error on this rank only): other ranks' positions unknown
@@ -257,9 +278,10 @@ def train(args) -> int:
                 inv = cnt.clamp_min(1.0).reciprocal()
             loss = model(tok, lab, inv)
             loss.backward()
-            ddp.finish()
+            reducer.finish()
             optimizer.clip_grad_norm_(args.grad_max_norm)
-            engine.fence()
+            if ckpt["engine"] is not None:
+                ckpt["engine"].fence()
             lr_now = optimizer.param_groups[0]["lr"]
             optimizer.step()
             lr_scheduler.step()
@@ -280,7 +302,7 @@ def train(args) -> int:
             training_step += 1
             losslog.flush()
             optimizer.check_finite(block=False)  # deferred non-finite check → error path
-            done = engine.poll()
+            done = ckpt["engine"].poll() if ckpt["engine"] is not None else None
             if done is not None:
                 logger.info(f"Checkpoint written: {done.path} ({done.bytes / 1e9:.2f} GB, "
                             f"stall {done.stall_s:.3f}s, durable after {done.total_s:.2f}s)")
@@ -296,7 +318,8 @@ def train(args) -> int:
         if device.type == "cuda":
             torch.cuda.synchronize()
         optimizer.check_finite(block=True)
-        engine.wait()
+        if ckpt["engine"] is not None:
+            ckpt["engine"].wait()
         logger.info("Training completed")
     except Exception as e:  # noqa: BLE001 - the reference catches everything here (train.py:121)
         losslog.flush(force=True)
@@ -307,13 +330,16 @@ def train(args) -> int:
         # the same step; any other error may be local to this rank
         collective = info.distributed and isinstance(e, (SignalInterrupt, InjectedFault))
         try:
-            engine.wait()
+            if ckpt["engine"] is not None:
+                ckpt["engine"].wait()
         except Exception as we:  # noqa: BLE001
             logger.error(f"previous checkpoint write failed: {we!r}")
 
         def _save():
             with monitor.blocked():
                 st = save_checkpoint(blocking=True, collective=collective or not info.distributed)
+            if st is False:
+                return False
             if st is not None:
                 logger.info(f"Checkpoint {st.path}: {st.bytes / 1e9:.2f} GB in {st.total_s:.2f}s "
                             f"(mode {st.mode})")

@@ -156,6 +156,13 @@ def build_parser() -> argparse.ArgumentParser:
         help="Gradient all-reduce bucket size in MiB (data parallel)",
     )
     parser.add_argument(
+        "--dp-mode",
+        type=str,
+        default="",
+        choices=["", "allreduce", "zero1"],
+        help="Data-parallel gradient mode (default zero1: reduce-scatter + sharded AdamW + all-gather)",
+    )
+    parser.add_argument(
         "--consensus-every",
         type=int,
         default=1,

@@ -32,17 +32,18 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, out_dir, bucket_mb):
+def _worker(rank, world, port, out_dir, bucket_mb, mode):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
     torch.set_num_threads(1)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from fault_tolerant_llm_training_amd.data.synthetic import SyntheticTokens
     from fault_tolerant_llm_training_amd.models.llama import build_model, model_args_for
-    from fault_tolerant_llm_training_amd.parallel.ddp import FlatDDP
+    from fault_tolerant_llm_training_amd.parallel.ddp import GradReducer
 
     a = model_args_for("tiny", vocab_size=128, seq_len=16)
     m = build_model(a, "cpu", torch.float32, seed=5)
-    ddp = FlatDDP(m.flat, m.sinks_in_backward_order(), bucket_mb=bucket_mb)
+    ddp = GradReducer(m.flat, m.sinks_in_backward_order(), bucket_mb=bucket_mb, mode=mode)
+    assert ddp.mode == mode
     ddp.broadcast_params()
     ds = SyntheticTokens(128, 16, seed=9, rank=rank, world_size=world, pin=False)
     for step in range(2):
@@ -53,18 +54,30 @@ def _worker(rank, world, port, out_dir, bucket_mb):
         loss = m(x, y, 1.0 / n)
         loss.backward()
         ddp.finish()
-    torch.save(m.flat.grads.clone(), os.path.join(out_dir, f"g{rank}.pt"))
+    if mode == "allreduce":
+        torch.save(m.flat.grads.clone(), os.path.join(out_dir, f"g{rank}.pt"))
+    else:  # scatter this rank's reduced shards back into a full-layout tensor
+        full = torch.full_like(m.flat.grads, float("nan"))
+        for b in ddp.buckets:
+            lo = b.lo + rank * b.shard_len
+            full[lo : lo + b.shard_len] = ddp.grad_shard[b.shard_lo : b.shard_lo + b.shard_len]
+        torch.save(full, os.path.join(out_dir, f"g{rank}.pt"))
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("bucket_mb", [0.05, 256.0])
-def test_ddp_grads_equal_single_process_global_batch(tmp_path, bucket_mb):
+@pytest.mark.parametrize("mode,bucket_mb", [("allreduce", 0.05), ("allreduce", 256.0), ("zero1", 0.05),
+                                             ("zero1", 256.0)])
+def test_ddp_grads_equal_single_process_global_batch(tmp_path, mode, bucket_mb):
     world = 2
-    mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path), bucket_mb), nprocs=world,
+    mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path), bucket_mb, mode), nprocs=world,
                        start_method="spawn")
     g0 = torch.load(tmp_path / "g0.pt")
     g1 = torch.load(tmp_path / "g1.pt")
-    assert torch.equal(g0, g1)
+    if mode == "allreduce":
+        assert torch.equal(g0, g1)
+    else:  # the two ranks own disjoint, complementary shards
+        assert not torch.isnan(torch.where(torch.isnan(g0), g1, g0)).any()
+        g0 = torch.where(torch.isnan(g0), g1, g0)
     from fault_tolerant_llm_training_amd.data.synthetic import SyntheticTokens
     from fault_tolerant_llm_training_amd.models.llama import build_model, model_args_for
 
@@ -107,15 +120,17 @@ def _rank_pids(parent_pid):
     return out
 
 
-def test_dp_signal_to_one_rank_stops_all_and_resume_is_exact(tmp_path):
+@pytest.mark.parametrize("mode", ["zero1", "allreduce"])
+def test_dp_signal_to_one_rank_stops_all_and_resume_is_exact(tmp_path, mode):
     d = str(tmp_path)
     write_fake_sbatch(d)
     ck = ["--checkpoint-path", os.path.join(d, "ck")]
-    base = TINY + ["--synthetic-data", "--vocab-size", "256", "--training-steps", "31", "--lr-warmup-steps", "3"] + ck
+    base = TINY + ["--synthetic-data", "--vocab-size", "256", "--training-steps", "31", "--lr-warmup-steps", "3",
+                   "--dp-mode", mode, "--dp-bucket-mb", "0.1"] + ck
     end = ["--raise-error", "--error-step", "30"]
     rc, out = _run(d, "100", base + end)
     assert rc == 0 and "Checkpoint saved at step 30" in out, out
-    assert "Data parallel over 2 ranks" in out
+    assert f"Data parallel over 2 ranks: {mode}" in out
 
     cmd, env = _torchrun(d, "200", base + end)
     log = open(os.path.join(d, "dp.log"), "w")

@@ -158,3 +158,40 @@ def test_tiny_model_gpu_vs_cpu():
     lc.backward()
     assert abs(lg.item() - lc.item()) < 2e-2
     assert rel(mg.flat.grads.cpu(), mc.flat.grads) < 3e-2
+
+
+@pytest.mark.parametrize("max_norm", [0.0, 1e-3])
+def test_pipelined_optimizer_matches_serial(max_norm):
+    """Side-stream sumsq + per-bucket AdamW gated into the next forward == one serial AdamW pass."""
+    from fault_tolerant_llm_training_amd.models.llama import build_model, model_args_for
+    from fault_tolerant_llm_training_amd.optim.adamw import FlatAdamW
+    from fault_tolerant_llm_training_amd.parallel.ddp import GradReducer
+
+    a = model_args_for("tiny", vocab_size=512, seq_len=64)
+    tok = torch.randint(0, 512, (2, 64), device="cuda")
+    lab = torch.randint(0, 512, (2, 64), device="cuda")
+    out = []
+    for pipelined in (False, True):
+        m = build_model(a, "cuda", torch.bfloat16, seed=11)
+        red = GradReducer(m.flat, m.sinks_in_backward_order(), bucket_mb=0.25) if pipelined else None
+        opt = FlatAdamW(m.parameters(), m.flat, lr=1e-2, max_grad_norm=max_norm, reducer=red)
+        m.gate = opt.gate
+        losses = []
+        for _ in range(3):
+            loss = m(tok, lab)
+            loss.backward()
+            if red is not None:
+                red.finish()
+            opt.step()
+            losses.append(loss.float())
+        opt.gate.wait_all()
+        torch.cuda.synchronize()
+        if pipelined:
+            assert len(red.buckets) > 3
+        out.append((m.flat.params.clone(), torch.stack(losses), opt.stats.clone()))
+    (p0, l0, s0), (p1, l1, s1) = out
+    assert torch.allclose(s0[0], s1[0], rtol=1e-5)
+    if max_norm == 0.0:
+        assert torch.equal(p0, p1) and torch.equal(l0, l1)
+    else:
+        assert rel(p0, p1) < 1e-3

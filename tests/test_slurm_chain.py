@@ -1,0 +1,44 @@
+"""The reference's Slurm job chain, end to end, through ``train.sh`` under the Slurm emulator.
+
+``--signal=USR1@lead`` → save → ``sbatch $WORKDIR/train.sh $SLURM_JOB_ID`` → next job gets
+``$1`` → ``--checkpoint-id`` → resumes; ×3 (BASELINE config 2, CPU-sized model).
+"""
+import os
+import re
+
+import pytest
+
+from fault_tolerant_llm_training_amd.ft.slurm_sim import SlurmSim
+
+from helpers import ROOT
+
+pytestmark = pytest.mark.slow
+
+
+def test_usr1_resubmit_chain_x3(tmp_path):
+    env = dict(os.environ)
+    env["EXTRA_TRAINING_ARGS"] = (f"--device cpu --model tiny --synthetic-data --vocab-size 256 --sequence-length 32 "
+                                  f"--training-steps 1000000 --error-step 1000000 --checkpoint-path {tmp_path}/ck "
+                                  f"--logging-frequency 50")
+    env["OMP_NUM_THREADS"] = "2"
+    env["PYTHONUNBUFFERED"] = "1"
+    sim = SlurmSim(ROOT, time_limit=14.0, signal_lead=7.0, kill_wait=20.0, env=env, log_dir=str(tmp_path))
+    first = sim.submit("train.sh")
+    jobs = sim.run(max_jobs=3)
+    assert [j.job_id for j in jobs] == [first, first + 1, first + 2]
+    prev_saved = None
+    for j in jobs:
+        out = open(j.log).read()
+        assert j.returncode == 0, out
+        assert j.signals[0] == "SIGUSR1", j.signals
+        assert "[EXIT HANDLER] Job timed out, saving checkpoint." in out, out
+        saved = int(re.search(r"Checkpoint saved at step (\d+)", out).group(1))
+        assert f"Submitted batch job {j.job_id + 1}" in out
+        if prev_saved is None:
+            assert "Starting training!" in out
+        else:  # zero steps lost across each preempt/resume
+            assert f"--checkpoint-id {j.job_id - 1}" not in out  # (argv is not logged verbatim)
+            assert f"checkpoint_id='{j.job_id - 1}'" in out
+            assert f"Resuming training from training_step {prev_saved}" in out, out
+            assert saved > prev_saved
+        prev_saved = saved
