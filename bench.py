@@ -42,7 +42,9 @@ def parse():
     ap.add_argument("--ckpt-dir", default="", help="also time one async checkpoint save into this dir")
     ap.add_argument("--device", default="cuda")
     ap.add_argument("--dp-mode", default="", choices=["", "allreduce", "zero1"])
-    ap.add_argument("--no-overlap", action="store_true", help="optimizer as a serial phase (A/B)")
+    ap.add_argument("--no-overlap", action="store_true", help="per-bucket optimizer as a serial phase (A/B)")
+    ap.add_argument("--whole-buffer-optimizer", action="store_true",
+                    help="1 GPU: one norm + one AdamW launch over the flat buffer after backward (A/B)")
     return ap.parse_args()
 
 
@@ -65,7 +67,12 @@ def main():
     model = build_model(margs, dev, torch.bfloat16, seed=1234)
     red = GradReducer(model.flat, model.sinks_in_backward_order(), bucket_mb=a.bucket_mb,
                       mode=a.dp_mode or None, overlap=not a.no_overlap)
-    opt = FlatAdamW(model.parameters(), model.flat, lr=5e-5, max_grad_norm=1.0, reducer=red)
+    if a.whole_buffer_optimizer and world == 1:
+        for snk in list(model.flat.sinks.values()) + model.sinks_in_backward_order():
+            snk.hook = None
+        red.finish = lambda: None
+    opt = FlatAdamW(model.parameters(), model.flat, lr=5e-5, max_grad_norm=1.0,
+                    reducer=None if (a.whole_buffer_optimizer and world == 1) else red)
     model.gate = opt.gate
     sched = build_lr_scheduler(opt, 100)
     red.broadcast_params()

@@ -11,7 +11,8 @@
 // and the write (one HBM read + one write per element). Backward writes
 // per-wave fp32 dW partials (no atomics → deterministic) that a column-parallel
 // kernel folds into the bf16 weight gradient, which is written straight into
-// the flat gradient buffer.
+// the flat gradient buffer. Backward grid: ~2 rows per wave so every CU gets
+// work (rows are independent; a 64-block grid left 3/4 of the chip idle).
 #include "torch_utils.h"
 
 namespace {
@@ -92,7 +93,7 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(
   const int lane = threadIdx.x & 63;
   const int slot = blockIdx.x * ROWS_PER_BLOCK + (threadIdx.x >> 6);
   const int nslots = gridDim.x * ROWS_PER_BLOCK;
-  uint4 wr[CH];
+  uint4 wr[CH];  // (N <= 8192: the LDS fold below needs N*4 bytes)
   float acc[CH][8];
   const uint4 z = make_uint4(0, 0, 0, 0);
 #pragma unroll
@@ -158,33 +159,58 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(
       }
     }
   }
-  float* part = dw_part + (size_t)slot * N;
+  // Fold the 4 waves' dW partials in LDS (fixed wave order: deterministic), then one
+  // coalesced fp32 row per block -> the column-sum kernel reads nblk rows, not 4*nblk.
+  extern __shared__ __attribute__((aligned(16))) float red[];  // [N]
+  const int wave = threadIdx.x >> 6;
+#pragma unroll 1
+  for (int w = 0; w < ROWS_PER_BLOCK; ++w) {
+    if (wave == w) {
 #pragma unroll
-  for (int c = 0; c < CH; ++c) {
-    const int idx = c * 512 + lane * 8;
-    if (idx < N) {
-      *reinterpret_cast<float4*>(part + idx) = make_float4(acc[c][0], acc[c][1], acc[c][2], acc[c][3]);
-      *reinterpret_cast<float4*>(part + idx + 4) = make_float4(acc[c][4], acc[c][5], acc[c][6], acc[c][7]);
+      for (int c = 0; c < CH; ++c) {
+        const int idx = c * 512 + lane * 8;
+        if (idx < N) {
+          float4* r4 = reinterpret_cast<float4*>(red + idx);
+          if (w == 0) {
+            r4[0] = make_float4(acc[c][0], acc[c][1], acc[c][2], acc[c][3]);
+            r4[1] = make_float4(acc[c][4], acc[c][5], acc[c][6], acc[c][7]);
+          } else {
+            float4 a = r4[0], b = r4[1];
+            a.x += acc[c][0]; a.y += acc[c][1]; a.z += acc[c][2]; a.w += acc[c][3];
+            b.x += acc[c][4]; b.y += acc[c][5]; b.z += acc[c][6]; b.w += acc[c][7];
+            r4[0] = a;
+            r4[1] = b;
+          }
+        }
+      }
     }
+    __syncthreads();
   }
+  float* part = dw_part + (size_t)blockIdx.x * N;
+  for (int i = threadIdx.x * 4; i < N; i += 256 * 4)
+    *reinterpret_cast<float4*>(part + i) = *reinterpret_cast<const float4*>(red + i);
 }
 
 // Column sums of a [P, N] fp32 slab -> bf16 dw (optionally accumulated).
-// Block = 64 columns x 4 row groups; fixed summation order (deterministic).
+// Block = 32 columns x 8 row groups (128-B row segments); fixed summation order
+// (deterministic). 128 blocks for N = 4096.
 __global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ part,
                                                      bf16_t* __restrict__ dw, int P, int N,
                                                      bool accumulate) {
-  __shared__ float red[4][64];
-  const int col = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int g = threadIdx.x >> 6;
+  __shared__ float red[8][33];
+  const int cl = threadIdx.x & 31, g = threadIdx.x >> 5;
+  const int col = blockIdx.x * 32 + cl;
   float s = 0.f;
   if (col < N) {
-    for (int p = g; p < P; p += 4) s += part[(size_t)p * N + col];
+#pragma unroll 4
+    for (int p = g; p < P; p += 8) s += part[(size_t)p * N + col];
   }
-  red[g][threadIdx.x & 63] = s;
+  red[g][cl] = s;
   __syncthreads();
   if (g == 0 && col < N) {
-    float t = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) t += red[k][cl];
     if (accumulate) t += bf2f(dw[col]);
     dw[col] = f2bf(t);
   }
@@ -213,8 +239,9 @@ void launch_bwd(const bf16_t* dy, const bf16_t* x, const bf16_t* w, const float*
                 int N, hipStream_t st) {
   const int chunks = (N + 511) / 512;
   dim3 grid(nblk), block(256);
-#define FT_NB(C)                                                                          \
-  hipLaunchKernelGGL((norm_bwd_kernel<C, LN>), grid, block, 0, st, dy, x, w, rstd, mean, dx, \
+  const size_t lds = (size_t)N * sizeof(float);
+#define FT_NB(C)                                                                            \
+  hipLaunchKernelGGL((norm_bwd_kernel<C, LN>), grid, block, lds, st, dy, x, w, rstd, mean, dx, \
                      dres, part, M, N)
   if (chunks <= 1) FT_NB(1);
   else if (chunks <= 2) FT_NB(2);
@@ -278,8 +305,9 @@ at::Tensor norm_bwd(const at::Tensor& dy, const at::Tensor& x, const at::Tensor&
     TORCH_CHECK(dres->numel() == x.numel(), "norm_bwd: dres shape mismatch");
     dr = cptr<bf16_t>(*dres);
   }
-  int nblk = std::max(1, std::min((M + ROWS_PER_BLOCK * 8 - 1) / (ROWS_PER_BLOCK * 8), 64));
-  auto part = at::empty({(long)nblk * ROWS_PER_BLOCK, N}, x.options().dtype(at::kFloat));
+  // ~2 rows per wave: enough blocks to cover all 256 CUs, few enough partial rows
+  int nblk = std::max(1, std::min((M + ROWS_PER_BLOCK * 2 - 1) / (ROWS_PER_BLOCK * 2), 256));
+  auto part = at::empty({(long)nblk, N}, x.options().dtype(at::kFloat));
   if (M > 0) {
     if (ln)
       launch_bwd<true>(cptr<bf16_t>(dy), cptr<bf16_t>(x), cptr<bf16_t>(w), cptr<float>(rstd),
@@ -291,8 +319,8 @@ at::Tensor norm_bwd(const at::Tensor& dy, const at::Tensor& x, const at::Tensor&
                         ft_stream());
     FT_LAUNCH_CHECK();
   }
-  hipLaunchKernelGGL(colsum_kernel, dim3((N + 63) / 64), dim3(256), 0, ft_stream(),
-                     cptr<float>(part), mptr<bf16_t>(dw), nblk * ROWS_PER_BLOCK, N, accumulate);
+  hipLaunchKernelGGL(colsum_kernel, dim3((N + 31) / 32), dim3(256), 0, ft_stream(),
+                     cptr<float>(part), mptr<bf16_t>(dw), M > 0 ? nblk : 0, N, accumulate);
   FT_LAUNCH_CHECK();
   return dx;
 }

@@ -138,7 +138,7 @@ void grad_norm_(const at::Tensor& grad, const at::Tensor& stats, double max_norm
 
 void adamw_(const at::Tensor& p, const at::Tensor& g, const at::Tensor& m, const at::Tensor& v,
             const at::Tensor& stats, double lr, double beta1, double beta2, double eps, double wd,
-            int64_t step) {
+            int64_t step, int64_t max_blocks) {
   FT_CHECK_CUDA(p);
   FT_CHECK_CONTIG(p);
   FT_CHECK_CONTIG(g);
@@ -155,7 +155,9 @@ void adamw_(const at::Tensor& p, const at::Tensor& g, const at::Tensor& m, const
   const float bc1 = 1.f - (float)std::pow(beta1, (double)step);
   const float bc2 = 1.f - (float)std::pow(beta2, (double)step);
   const float inv_bc1 = 1.f / bc1, inv_sqrt_bc2 = 1.f / std::sqrt(bc2);
-  const dim3 grid(stream_grid(n8)), block(256);
+  int nb = stream_grid(n8);
+  if (max_blocks > 0) nb = std::max(1, std::min(nb, (int)max_blocks));
+  const dim3 grid(nb), block(256);
 #define FT_ADAM(PT, ST)                                                                            \
   hipLaunchKernelGGL((adamw_kernel<PT, ST>), grid, block, 0, ft_stream(), mptr<PT>(p), cptr<PT>(g), \
                      mptr<ST>(m), mptr<ST>(v), n8, (float)lr, (float)beta1, (float)beta2,          \
@@ -209,6 +211,6 @@ TORCH_LIBRARY_FRAGMENT(ftamd, m) {
   m.def("grad_norm_(Tensor grad, Tensor(a!) stats, float max_norm) -> ()", &grad_norm_);
   m.def(
       "adamw_(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, Tensor stats, float lr, float "
-      "beta1, float beta2, float eps, float wd, int step) -> ()",
+      "beta1, float beta2, float eps, float wd, int step, int max_blocks=0) -> ()",
       &adamw_);
 }

@@ -34,12 +34,13 @@ PYBIND11_MODULE(_runtime, m) {
       .def_readonly("fsync_seconds", &ZipStats::fsync_seconds)
       .def_readonly("wait_seconds", &ZipStats::wait_seconds)
       .def_readonly("bytes", &ZipStats::bytes)
+      .def_readonly("direct_bytes", &ZipStats::direct_bytes)
       .def_readonly("error", &ZipStats::error);
 
   py::class_<ZipWriter>(m, "ZipWriter")
-      .def(py::init<std::string, std::string, std::string, int, uint64_t>(), py::arg("tmp_path"),
+      .def(py::init<std::string, std::string, std::string, int, uint64_t, bool>(), py::arg("tmp_path"),
            py::arg("final_path"), py::arg("archive"), py::arg("nthreads") = 8,
-           py::arg("chunk_bytes") = (64ull << 20))
+           py::arg("chunk_bytes") = (64ull << 20), py::arg("direct") = true)
       .def("add_bytes",
            [](ZipWriter& w, const std::string& name, py::bytes b) { w.add_bytes(name, std::string(b)); })
       .def("add_buffer", &ZipWriter::add_buffer)

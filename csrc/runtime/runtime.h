@@ -44,13 +44,14 @@ struct ZipRecord {
 struct ZipStats {
   double seconds = 0, write_seconds = 0, fsync_seconds = 0, wait_seconds = 0;
   uint64_t bytes = 0;
+  uint64_t direct_bytes = 0;  // written with O_DIRECT
   std::string error;
 };
 
 class ZipWriter {
  public:
   ZipWriter(std::string tmp_path, std::string final_path, std::string archive, int nthreads,
-            uint64_t chunk_bytes);
+            uint64_t chunk_bytes, bool direct = true);
   ~ZipWriter();
   void add_bytes(const std::string& name, const std::string& bytes);
   void add_buffer(const std::string& name, uintptr_t ptr, uint64_t nbytes);
@@ -71,6 +72,8 @@ class ZipWriter {
   std::vector<ZipRecord> recs_;
   uint64_t cd_off_ = 0;
   bool laid_out_ = false;
+  bool direct_ = true;       // align big records and try O_DIRECT
+  bool direct_used_ = true;
   std::thread th_;
   std::atomic<bool> done_{false};
   ZipStats stats_;

@@ -35,7 +35,7 @@ def time_checkpoint_save(model, optimizer, lr_scheduler, ckpt_dir: str, info, mo
     st = eng.save(path, lambda host: build_checkpoint(model, optimizer, lr_scheduler, 0, host), blocking=False)
     enq = time.perf_counter() - t0
     eng.fence()  # what the next optimizer step would wait for
-    torch.cuda.synchronize()
+    torch.cuda.current_stream().synchronize()  # (not the side stream's D2H drain)
     stall = time.perf_counter() - t0
     st = eng.wait()
     total = time.perf_counter() - t0
@@ -47,6 +47,7 @@ def time_checkpoint_save(model, optimizer, lr_scheduler, ckpt_dir: str, info, mo
         "drain_wait_s": round(st.drain_wait_s, 3),
         "write_s": round(st.write_s, 3),
         "fsync_s": round(st.fsync_s, 3),
+        "direct_GB": round(st.direct_bytes / 1e9, 2),
         "total_s": round(total, 3),
         "GB_per_s": round(st.bytes / total / 1e9, 2),
         "pinned_alloc_s": round(alloc_s, 3),

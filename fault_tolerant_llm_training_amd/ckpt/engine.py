@@ -50,6 +50,7 @@ class SaveStats:
     drain_wait_s: float = 0.0    # writer thread waiting for the D2H drain
     write_s: float = 0.0         # CRC + pwrite
     fsync_s: float = 0.0         # fsync + rename (+ dir fsync)
+    direct_bytes: int = 0        # bytes written with O_DIRECT from the pinned snapshot
     total_s: float = 0.0         # save() call → file durable
     error: str = ""
 
@@ -236,6 +237,7 @@ class CheckpointEngine:
             ws = inf.writer.wait()
             st.drain_wait_s, st.write_s, st.fsync_s = ws.wait_seconds, ws.write_seconds, ws.fsync_seconds
             st.bytes = ws.bytes or st.bytes
+            st.direct_bytes = ws.direct_bytes
             if ws.error:
                 st.error = ws.error
         if inf.thread is not None:

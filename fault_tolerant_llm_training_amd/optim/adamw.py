@@ -28,6 +28,7 @@ A non-finite norm makes every update kernel skip (no host sync);
 from __future__ import annotations
 
 import math
+import os
 from typing import List, Optional, Tuple
 
 import torch
@@ -101,6 +102,9 @@ class FlatAdamW(torch.optim.Optimizer):
         self._stats_event = None
         self._stats_step = -1
         self.gate = ParamGate()
+        # grid cap for the per-bucket AdamW launches that run concurrently with the next
+        # forward's GEMMs (fewer blocks = less contention for CU issue slots)
+        self.overlap_blocks = int(os.environ.get("FT_ADAMW_BLOCKS", "0"))
         # parameter index (reference order) -> flat slot
         name_of = {id(p): n for n, p in flat.param_objs.items()}
         self._index_slots = [flat.slots[name_of[id(p)]] for p in params]
@@ -126,9 +130,9 @@ class FlatAdamW(torch.optim.Optimizer):
         b1, b2 = grp["betas"]
         return float(grp["lr"]), b1, b2, grp["eps"], grp["weight_decay"]
 
-    def _update(self, p, g, m, v, lr, b1, b2, eps, wd):
+    def _update(self, p, g, m, v, lr, b1, b2, eps, wd, max_blocks: int = 0):
         if p.is_cuda:
-            kernels().adamw_(p, g, m, v, self.stats, lr, b1, b2, eps, wd, self.step_count)
+            kernels().adamw_(p, g, m, v, self.stats, lr, b1, b2, eps, wd, self.step_count, max_blocks)
         else:
             _adamw_reference(p, g, m, v, self.stats, lr, b1, b2, eps, wd, self.step_count)
 
@@ -160,7 +164,8 @@ class FlatAdamW(torch.optim.Optimizer):
             for b in sorted(r.buckets, key=lambda b: b.lo):  # forward order
                 slo, shi = r.state_range(b)
                 self._update(r.param_for_update(b), r.grad_for_update(b), self.exp_avg[slo:shi],
-                             self.exp_avg_sq[slo:shi], lr, b1, b2, eps, wd)
+                             self.exp_avg_sq[slo:shi], lr, b1, b2, eps, wd,
+                             self.overlap_blocks if r.overlap else 0)
                 if self.zero1:
                     work = dist.all_gather_into_tensor(f.params[b.lo : b.hi], r.param_shard(b),
                                                        group=r.group, async_op=True)

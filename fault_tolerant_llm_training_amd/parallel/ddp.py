@@ -45,7 +45,7 @@ from ..models.flat import FlatParamSpace
 from ..ops.grad_sink import GradSink
 
 MODES = ("local", "allreduce", "zero1")
-PARTIALS_PER_BUCKET = 128
+PARTIALS_PER_BUCKET = 512
 
 
 class Bucket:
@@ -92,12 +92,13 @@ class GradReducer:
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        explicit = mode is not None
         if mode is None:
             mode = "local" if self.world == 1 else "zero1"
         if mode not in MODES:
             raise ValueError(f"unknown gradient mode {mode!r}")
-        if self.world == 1:
-            mode = "local"
+        if self.world == 1 and not (explicit and dist.is_initialized()):
+            mode = "local"  # (an explicit mode on a 1-rank process group exercises the collective path)
         if mode == "zero1" and flat.align % (8 * self.world):
             mode = "allreduce"  # shards must stay 8-element aligned for the vector kernels
         self.mode = mode
@@ -129,7 +130,7 @@ class GradReducer:
                 b.event = torch.cuda.Event()
         for sink in list(flat.sinks.values()) + list(extra_sinks):
             sink.hook = self._on_ready
-        self.comm = self.world > 1
+        self.comm = self.world > 1 or mode != "local"
 
     # ---------------------------------------------------------------- shard views
     def param_shard(self, b: Bucket) -> torch.Tensor:

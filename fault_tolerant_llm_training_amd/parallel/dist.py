@@ -35,7 +35,7 @@ class DistInfo:
 
     @property
     def distributed(self) -> bool:
-        return self.world_size > 1
+        return self.world_size > 1 or self.ctrl_group is not None
 
 
 _INFO: Optional[DistInfo] = None
@@ -61,7 +61,8 @@ def init_distributed(device_type: str = "cuda", timeout_s: int = 1800) -> DistIn
     else:
         device = torch.device("cpu")
     info = DistInfo(rank, world, local, device)
-    if world > 1:
+    # FT_FORCE_DIST=1 builds the process groups even for one rank (exercises the RCCL path on 1 GPU)
+    if world > 1 or os.environ.get("FT_FORCE_DIST") == "1":
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29500")
         os.environ["RANK"], os.environ["WORLD_SIZE"] = str(rank), str(world)
