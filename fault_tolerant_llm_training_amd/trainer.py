@@ -260,11 +260,21 @@ def train(args) -> int:
         inv_static = torch.full((1,), 1.0 / (B * S * W), dtype=torch.float32, device=device)
     t_window, steps_window = time.perf_counter(), 0
     logger.info(f"Setup took {time.perf_counter() - t_setup:.2f}s")
+    prof, prof_range = None, None
+    if args.profile_steps:
+        a0, a1 = (int(v) for v in args.profile_steps.split(":"))
+        prof_range = (a0, a1)
 
     try:
         while training_step < args.training_steps:
             if args.raise_error and training_step == args.error_step:
                 raise InjectedFault()
+            if prof_range is not None and training_step == prof_range[0] and prof is None:
+                acts = [torch.profiler.ProfilerActivity.CPU]
+                if device.type == "cuda":
+                    acts.append(torch.profiler.ProfilerActivity.CUDA)
+                prof = torch.profiler.profile(activities=acts, record_shapes=True)
+                prof.__enter__()
             batch = next(loader)
             tok = batch.inputs.to(device, non_blocking=True)
             lab = batch.labels.to(device, non_blocking=True)
@@ -294,12 +304,23 @@ def train(args) -> int:
                 extra = {"step_ms": f"{dt * 1e3:.1f}", "tok/s": f"{tok_s:.0f}",
                          "MFU": f"{tok_s / W * fpt / 2.5e15:.3f}" if device.type == "cuda" else "n/a",
                          "lr": f"{lr_now:.3e}"}
+                if device.type == "cuda":
+                    extra["peak_HBM_GB"] = f"{torch.cuda.max_memory_allocated(device) / 2**30:.1f}"
                 losslog.push(training_step, loss, extra)
                 if metrics_f is not None:
                     metrics_f.write(json.dumps({"step": training_step, "step_ms": dt * 1e3, "tok_s": tok_s}) + "\n")
                     metrics_f.flush()
                 t_window, steps_window = now, 0
             training_step += 1
+            if prof is not None and training_step >= prof_range[1]:
+                if device.type == "cuda":
+                    torch.cuda.synchronize()
+                prof.__exit__(None, None, None)
+                os.makedirs(args.profile_dir, exist_ok=True)
+                out = os.path.join(args.profile_dir, f"trace_rank{info.rank}_steps{prof_range[0]}-{prof_range[1]}.json")
+                prof.export_chrome_trace(out)
+                logger.info(f"torch.profiler trace written to {out}")
+                prof, prof_range = None, None
             losslog.flush()
             optimizer.check_finite(block=False)  # deferred non-finite check → error path
             done = ckpt["engine"].poll() if ckpt["engine"] is not None else None

@@ -169,6 +169,13 @@ def build_parser() -> argparse.ArgumentParser:
         help="Agree on pending stop signals across ranks every N steps",
     )
     parser.add_argument(
+        "--profile-steps",
+        type=str,
+        default="",
+        help="torch.profiler window 'START:STOP' (steps); Chrome trace written to --profile-dir",
+    )
+    parser.add_argument("--profile-dir", type=str, default="profiles/torch", help="Output dir for --profile-steps")
+    parser.add_argument(
         "--metrics-file", type=str, default="", help="Append per-step JSON metrics to this file"
     )
     parser.add_argument(

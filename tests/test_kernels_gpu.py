@@ -195,3 +195,21 @@ def test_pipelined_optimizer_matches_serial(max_norm):
         assert torch.equal(p0, p1) and torch.equal(l0, l1)
     else:  # the norm's partial-sum split differs -> clip coefficient differs in the last bits
         assert rel(p0, p1) < 1e-2 and rel(s0[:1], s1[:1]) < 1e-2
+
+
+@pytest.mark.parametrize("R,C", [(64, 64), (2048, 4096), (128, 28672), (4096, 192)])
+def test_transpose2d(K, R, C):
+    x = torch.randn(R, C, device="cuda").bfloat16()
+    assert torch.equal(K.transpose2d(x), x.t().contiguous())
+
+
+@pytest.mark.parametrize("mode", ["all", "none"])
+def test_weight_grad_layouts(mode, monkeypatch):
+    from fault_tolerant_llm_training_amd.ops import functional as Fx
+
+    monkeypatch.setattr(Fx, "_DW_MODE", mode)
+    dy = torch.randn(256, 384, device="cuda").bfloat16()
+    x = torch.randn(256, 128, device="cuda").bfloat16()
+    dw = Fx.weight_grad(dy, x, None)
+    ref = dy.float().t() @ x.float()
+    assert rel(dw, ref) < 1e-2
