@@ -339,7 +339,9 @@ __global__ __launch_bounds__(256) void flash_bwd_pre_kernel(const bf16_t* __rest
   }
 }
 
-template <int D>
+// DQ: 0 = dQ by fp32 atomics (default), 1 = no dQ stage (dK/dV only; a separate
+// deterministic dQ kernel follows), 2 = timing experiment: plain (racy) stores.
+template <int D, int DQ = 0>
 __global__ __launch_bounds__(256, 1) void flash_bwd_kernel(
     const bf16_t* __restrict__ dO, const bf16_t* __restrict__ qk, const bf16_t* __restrict__ qkv,
     const float* __restrict__ lse2, const float* __restrict__ delta, float* __restrict__ dq_acc,
@@ -496,7 +498,7 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_kernel(
     __syncthreads();
     if (more) BWD_GLDS(qs + 1, cur ^ 1)
     // dQ[q, d] += scale * sum_keys dS[q, key] K[key, d]
-    {
+    if constexpr (DQ != 1) {
       f32x16_t acc;
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[r] = 0.f;
@@ -512,7 +514,11 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_kernel(
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int q = qb + (r & 3) + 8 * (r >> 2) + 4 * hi;
-          if (q < S) atomicAdd(dq_acc + ((long)b * S + q) * ldo + (long)h * D + d, acc[r] * scale);
+          if constexpr (DQ == 0) {
+            if (q < S) atomicAdd(dq_acc + ((long)b * S + q) * ldo + (long)h * D + d, acc[r] * scale);
+          } else {
+            if (q < S) dq_acc[((long)b * S + q) * ldo + (long)h * D + d] = acc[r] * scale;
+          }
         }
       }
     }
@@ -536,6 +542,155 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_kernel(
     }
 }
 
+// ================================================================== backward dQ (deterministic)
+// Q-major like the forward: per wave 32 query rows, sweep 64-key tiles up to the
+// diagonal; S^T = K Q^T and dP^T = V dO^T (A = K / V rows from LDS, B = Q^T / dO^T
+// in VGPRs), dS^T = P^T (dP^T - delta) with P = exp2(S^T*c - lse2) (the query is on
+// the lane, so lse/delta are per-lane scalars), dQ^T += K^T dS^T (A = K^T through
+// transposed LDS reads, B = dS^T straight from the accumulators). Every dQ element
+// is produced by exactly one wave in a fixed order: no atomics, bit-reproducible.
+// Used with flash_bwd_kernel<D, 1> (dK/dV only) for --deterministic runs.
+template <int D>
+__global__ __launch_bounds__(256, 1) void flash_bwd_dq_kernel(
+    const bf16_t* __restrict__ dO, const bf16_t* __restrict__ qk, const bf16_t* __restrict__ qkv,
+    const float* __restrict__ lse2, const float* __restrict__ delta, bf16_t* __restrict__ dqkv, int B,
+    int S, int Hq, int Hkv, float sl2, float scale) {
+  constexpr int BM = 128, BN = 64, KS = D / 16, NDB = D / 32, DCH = D / 8;
+  constexpr int TILE = BN * D * 2;
+  constexpr int CPT = BN * DCH / 256;
+  __shared__ __attribute__((aligned(16))) char smem[4 * TILE];
+
+  const int nqt = (S + BM - 1) / BM;
+  const int per = B * Hq;
+  const int L = blockIdx.x;
+  const int qt = nqt - 1 - L / per;
+  const int rem = L % per;
+  const int b = rem / Hq;
+  int h, kvh;
+  map_head(rem % Hq, Hq, Hkv, h, kvh);
+
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, l32 = lane & 31, hi = lane >> 5;
+  const int q0 = qt * BM + wave * 32;
+  const int qrow = q0 + l32;
+  const long ldqk = (long)(Hq + Hkv) * D, ldv = (long)(Hq + 2 * Hkv) * D, ldo = (long)Hq * D;
+  const bf16_t* Qg = qk + (long)b * S * ldqk + (long)h * D;
+  const bf16_t* Kg = qk + (long)b * S * ldqk + (long)(Hq + kvh) * D;
+  const bf16_t* Vg = qkv + (long)b * S * ldv + (long)(Hq + Hkv + kvh) * D;
+  const bf16_t* dOg = dO + (long)b * S * ldo + (long)h * D;
+
+  bf16x8_t qf[KS], df[KS];
+  const long qr = min(qrow, S - 1);
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    qf[ks] = *reinterpret_cast<const bf16x8_t*>(Qg + qr * ldqk + ks * 16 + hi * 8);
+    df[ks] = *reinterpret_cast<const bf16x8_t*>(dOg + qr * ldo + ks * 16 + hi * 8);
+  }
+  const float lq = lse2[((long)b * Hq + h) * S + qr];
+  const float dlq = delta[((long)b * Hq + h) * S + qr];
+
+  const int kend = min((qt + 1) * BM, S);
+  const int ntiles = (kend + BN - 1) / BN;
+  u32x4 kr[CPT], vr[CPT];
+#define DQ_GLOAD(KT)                                                         \
+  static_for<CPT>([&](auto I) {                                              \
+    const int id = tid + I * 256, row = id / DCH, c = id % DCH;              \
+    const long key = min((KT) * BN + row, S - 1);                            \
+    kr[I] = *reinterpret_cast<const u32x4*>(Kg + key * ldqk + c * 8);        \
+    vr[I] = *reinterpret_cast<const u32x4*>(Vg + key * ldv + c * 8);         \
+  });
+#define DQ_SWRITE(BUF)                                                       \
+  static_for<CPT>([&](auto I) {                                              \
+    const int id = tid + I * 256, row = id / DCH, c = id % DCH;              \
+    char* kb_ = smem + (BUF) * 2 * TILE;                                     \
+    *reinterpret_cast<u32x4*>(kb_ + lds_off<D>(row, c)) = kr[I];             \
+    *reinterpret_cast<u32x4*>(kb_ + TILE + lds_off<D>(row, c)) = vr[I];      \
+  });
+
+  DQ_GLOAD(0)
+  DQ_SWRITE(0)
+  __syncthreads();
+
+  f32x16_t dq[NDB];
+#pragma unroll
+  for (int db = 0; db < NDB; ++db)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dq[db][r] = 0.f;
+
+  for (int kt = 0; kt < ntiles; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < ntiles) {
+      DQ_GLOAD(kt + 1)
+    }
+    const char* kb = smem + cur * 2 * TILE;
+    const char* vb = kb + TILE;
+    const int k0 = kt * BN;
+    const bool v0 = k0 <= q0 + 31;
+    const bool v1 = k0 + 32 <= q0 + 31;
+    if (v0) {
+      f32x16_t sc[2], dp[2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sc[j][r] = dp[j][r] = 0.f;
+        if (j == 0 || v1) {
+#pragma unroll
+          for (int ks = 0; ks < KS; ++ks) {
+            sc[j] = mfma32(ld_row<D>(kb, j * 32 + l32, 2 * ks + hi), qf[ks], sc[j]);
+            dp[j] = mfma32(ld_row<D>(vb, j * 32 + l32, 2 * ks + hi), df[ks], dp[j]);
+          }
+        }
+      }
+      const bool diag = k0 + BN - 1 > q0;
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          float p = exp2f(sc[j][r] * sl2 - lq);
+          if (j == 1 && !v1) p = 0.f;
+          if (diag) {
+            const int key = k0 + j * 32 + (r & 3) + 8 * (r >> 2) + 4 * hi;
+            if (key > qrow) p = 0.f;
+          }
+          if (qrow >= S) p = 0.f;
+          sc[j][r] = p * (dp[j][r] - dlq);
+        }
+      const bf16x8_t d00 = cvt8<0>(sc[0]), d01 = cvt8<8>(sc[0]);
+      const bf16x8_t d10 = cvt8<0>(sc[1]), d11 = cvt8<8>(sc[1]);
+#pragma unroll
+      for (int db = 0; db < NDB; ++db) {
+        dq[db] = mfma32(tr_frag<D>(kb, 0, db * 32, lane), d00, dq[db]);
+        dq[db] = mfma32(tr_frag<D>(kb, 16, db * 32, lane), d01, dq[db]);
+      }
+      if (v1) {
+#pragma unroll
+        for (int db = 0; db < NDB; ++db) {
+          dq[db] = mfma32(tr_frag<D>(kb, 32, db * 32, lane), d10, dq[db]);
+          dq[db] = mfma32(tr_frag<D>(kb, 48, db * 32, lane), d11, dq[db]);
+        }
+      }
+    }
+    if (kt + 1 < ntiles) {
+      DQ_SWRITE(cur ^ 1)
+    }
+    __syncthreads();
+  }
+#undef DQ_GLOAD
+#undef DQ_SWRITE
+
+  if (qrow < S) {
+    bf16_t* orow = dqkv + ((long)b * S + qrow) * ldv + (long)h * D;
+#pragma unroll
+    for (int db = 0; db < NDB; ++db)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        uint2 v;
+        v.x = pack2(dq[db][4 * g + 0] * scale, dq[db][4 * g + 1] * scale);
+        v.y = pack2(dq[db][4 * g + 2] * scale, dq[db][4 * g + 3] * scale);
+        *reinterpret_cast<uint2*>(orow + db * 32 + 8 * g + 4 * hi) = v;
+      }
+  }
+}
+
 // dqkv[:, q | k | v] = bf16(dQ), bf16(sum_G dK_part), bf16(sum_G dV_part)
 __global__ __launch_bounds__(256) void flash_bwd_finalize_kernel(
     const float* __restrict__ dq_acc, const float* __restrict__ dk_part,
@@ -549,6 +704,7 @@ __global__ __launch_bounds__(256) void flash_bwd_finalize_kernel(
     const int col = (int)(i - t * vpr) * 4;
     float4 v;
     if (col < Hq * D) {
+      if (dq_acc == nullptr) continue;  // dQ already written by the deterministic dQ kernel
       v = *reinterpret_cast<const float4*>(dq_acc + t * Hq * D + col);
     } else {
       const bool isk = col < (Hq + Hkv) * D;
@@ -612,7 +768,7 @@ std::tuple<at::Tensor, at::Tensor> flash_fwd(const at::Tensor& qk, const at::Ten
 // Returns dqkv [T, (Hq+2Hkv)*D] bf16 (dQ/dK in the rotated frame; RoPE backward follows).
 at::Tensor flash_bwd(const at::Tensor& dout, const at::Tensor& qk, const at::Tensor& qkv,
                      const at::Tensor& out, const at::Tensor& lse, int64_t S, int64_t Hq,
-                     int64_t Hkv, int64_t D) {
+                     int64_t Hkv, int64_t D, int64_t mode) {
   check_inputs(qk, qkv, S, Hq, Hkv, D);
   FT_CHECK_CONTIG(dout);
   FT_CHECK_CONTIG(out);
@@ -623,7 +779,11 @@ at::Tensor flash_bwd(const at::Tensor& dout, const at::Tensor& qk, const at::Ten
   const at::DeviceGuard guard(qk.device());
   auto f32 = qk.options().dtype(at::kFloat);
   auto delta = at::empty({B, Hq, S}, f32);
-  auto dq_acc = at::zeros({T, Hq * D}, f32);
+  // mode 0: dQ by fp32 atomics in the KV-major kernel (fastest);
+  // mode 1: deterministic — KV kernel without dQ + Q-major dQ kernel (no atomics);
+  // mode 2: timing experiment only (racy dQ stores).
+  const bool det = mode == 1;
+  at::Tensor dq_acc = det ? at::Tensor() : (mode == 2 ? at::empty({T, Hq * D}, f32) : at::zeros({T, Hq * D}, f32));
   auto dk_part = at::empty({T, Hq * D}, f32);
   auto dv_part = at::empty({T, Hq * D}, f32);
   auto dqkv = at::empty({T, (Hq + 2 * Hkv) * D}, qk.options());
@@ -633,26 +793,36 @@ at::Tensor flash_bwd(const at::Tensor& dout, const at::Tensor& qk, const at::Ten
   const int pre_blocks = (int)((rows * 16 + 255) / 256);
   const int nkt = (S + 127) / 128;
   dim3 grid(nkt * B * Hq), block(256);
+  float* dqp = det ? nullptr : mptr<float>(dq_acc);
+#define FT_BWD(DD, MODE)                                                                          \
+  hipLaunchKernelGGL((flash_bwd_kernel<DD, MODE>), grid, block, 0, ft_stream(), cptr<bf16_t>(dout), \
+                     cptr<bf16_t>(qk), cptr<bf16_t>(qkv), cptr<float>(lse), cptr<float>(delta),     \
+                     dqp, mptr<float>(dk_part), mptr<float>(dv_part), B, (int)S, (int)Hq, (int)Hkv, \
+                     sl2, scale)
+#define FT_DQ(DD)                                                                                  \
+  hipLaunchKernelGGL((flash_bwd_dq_kernel<DD>), dim3(nkt * B * Hq), block, 0, ft_stream(),          \
+                     cptr<bf16_t>(dout), cptr<bf16_t>(qk), cptr<bf16_t>(qkv), cptr<float>(lse),     \
+                     cptr<float>(delta), mptr<bf16_t>(dqkv), B, (int)S, (int)Hq, (int)Hkv, sl2, scale)
   if (D == 128) {
     hipLaunchKernelGGL(flash_bwd_pre_kernel<128>, dim3(pre_blocks), block, 0, ft_stream(),
                        cptr<bf16_t>(dout), cptr<bf16_t>(out), mptr<float>(delta), B, (int)S, (int)Hq);
-    hipLaunchKernelGGL(flash_bwd_kernel<128>, grid, block, 0, ft_stream(), cptr<bf16_t>(dout),
-                       cptr<bf16_t>(qk), cptr<bf16_t>(qkv), cptr<float>(lse), cptr<float>(delta),
-                       mptr<float>(dq_acc), mptr<float>(dk_part), mptr<float>(dv_part), B, (int)S,
-                       (int)Hq, (int)Hkv, sl2, scale);
+    if (mode == 0) FT_BWD(128, 0);
+    else if (mode == 1) { FT_BWD(128, 1); FT_DQ(128); }
+    else FT_BWD(128, 2);
   } else {
     hipLaunchKernelGGL(flash_bwd_pre_kernel<64>, dim3(pre_blocks), block, 0, ft_stream(),
                        cptr<bf16_t>(dout), cptr<bf16_t>(out), mptr<float>(delta), B, (int)S, (int)Hq);
-    hipLaunchKernelGGL(flash_bwd_kernel<64>, grid, block, 0, ft_stream(), cptr<bf16_t>(dout),
-                       cptr<bf16_t>(qk), cptr<bf16_t>(qkv), cptr<float>(lse), cptr<float>(delta),
-                       mptr<float>(dq_acc), mptr<float>(dk_part), mptr<float>(dv_part), B, (int)S,
-                       (int)Hq, (int)Hkv, sl2, scale);
+    if (mode == 0) FT_BWD(64, 0);
+    else if (mode == 1) { FT_BWD(64, 1); FT_DQ(64); }
+    else FT_BWD(64, 2);
   }
+#undef FT_BWD
+#undef FT_DQ
   FT_LAUNCH_CHECK();
   const long vec = (long)T * ((Hq + 2 * Hkv) * D / 4);
   const int fin_blocks = (int)std::max(1L, std::min((vec + 255) / 256, 4096L));
   hipLaunchKernelGGL(flash_bwd_finalize_kernel, dim3(fin_blocks), block, 0, ft_stream(),
-                     cptr<float>(dq_acc), cptr<float>(dk_part), cptr<float>(dv_part),
+                     det ? nullptr : cptr<float>(dq_acc), cptr<float>(dk_part), cptr<float>(dv_part),
                      mptr<bf16_t>(dqkv), (long)T, (int)Hq, (int)Hkv, (int)D);
   FT_LAUNCH_CHECK();
   return dqkv;
@@ -663,6 +833,6 @@ TORCH_LIBRARY_FRAGMENT(ftamd, m) {
         &flash_fwd);
   m.def(
       "flash_bwd(Tensor dout, Tensor qk, Tensor qkv, Tensor out, Tensor lse, int S, int Hq, int "
-      "Hkv, int D) -> Tensor",
+      "Hkv, int D, int mode=0) -> Tensor",
       &flash_bwd);
 }

@@ -11,9 +11,20 @@ from __future__ import annotations
 import torch
 import torch.nn.functional as F
 
+import os
+
 from .._native import kernels
 
 _USE_HIP_FLASH = True
+# Backward variant: 0 = dQ accumulated with fp32 atomics inside the KV-major kernel
+# (fastest), 1 = deterministic (KV-major dK/dV + Q-major dQ kernel, no atomics, bit
+# reproducible — what resume-equivalence on the GPU needs).
+_BWD_MODE = int(os.environ.get("FT_FLASH_BWD_MODE", "0"))
+
+
+def set_deterministic(flag: bool) -> None:
+    global _BWD_MODE
+    _BWD_MODE = 1 if flag else 0
 
 
 def _split(qk, qkv, S, hq, hkv, d):
@@ -42,7 +53,7 @@ def flash_attn_fwd(qk, qkv, S, hq, hkv, d):
 def flash_attn_bwd(do, qk, qkv, o, lse, S, hq, hkv, d):
     """Returns dqkv [T, (Hq+2Hkv)*D] with dQ/dK still in the rotated frame."""
     if _USE_HIP_FLASH and hasattr(kernels(), "flash_bwd"):
-        return kernels().flash_bwd(do, qk, qkv, o, lse, S, hq, hkv, d)
+        return kernels().flash_bwd(do, qk, qkv, o, lse, S, hq, hkv, d, _BWD_MODE)
     with torch.enable_grad():
         qk_ = qk.detach().requires_grad_(True)
         qkv_ = qkv.detach().requires_grad_(True)

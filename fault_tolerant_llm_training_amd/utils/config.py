@@ -169,6 +169,11 @@ def build_parser() -> argparse.ArgumentParser:
         help="Agree on pending stop signals across ranks every N steps",
     )
     parser.add_argument(
+        "--deterministic",
+        action="store_true",
+        help="Bit-reproducible GPU kernels (atomic-free flash-attention dQ); resume is then bit-exact",
+    )
+    parser.add_argument(
         "--profile-steps",
         type=str,
         default="",

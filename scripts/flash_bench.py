@@ -1,0 +1,32 @@
+"""Flash attention fwd / bwd timing on the Llama-3-8B layer shape (B=1, S=2048, 32/8 heads, d=128)."""
+import torch
+
+from fault_tolerant_llm_training_amd._native import kernels
+
+K = kernels()
+S, Hq, Hkv, D = 2048, 32, 8, 128
+qkv = torch.randn(S, (Hq + 2 * Hkv) * D, device="cuda").bfloat16()
+qk = torch.randn(S, (Hq + Hkv) * D, device="cuda").bfloat16()
+do = torch.randn(S, Hq * D, device="cuda").bfloat16()
+o, lse = K.flash_fwd(qk, qkv, S, Hq, Hkv, D)
+unit = 2 * S * S / 2 * D * 2 * Hq  # one causal matmul, flops
+
+
+def t(fn, it=20):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(it):
+        fn()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / it * 1e3
+
+
+tf = t(lambda: K.flash_fwd(qk, qkv, S, Hq, Hkv, D))
+print(f"fwd {tf:7.1f} us  {2 * unit / tf / 1e6:6.0f} TF/s")
+for mode, name in ((0, "bwd atomics"), (1, "bwd deterministic"), (2, "bwd no-atomic (racy, timing only)")):
+    tb = t(lambda: K.flash_bwd(do, qk, qkv, o, lse, S, Hq, Hkv, D, mode))
+    print(f"{name:34s} {tb:7.1f} us  {5 * unit / tb / 1e6:6.0f} TF/s (5-matmul count)")
