@@ -16,10 +16,11 @@ import os
 from .._native import kernels
 
 _USE_HIP_FLASH = True
-# Backward variant: 0 = dQ accumulated with fp32 atomics inside the KV-major kernel
-# (fastest), 1 = deterministic (KV-major dK/dV + Q-major dQ kernel, no atomics, bit
-# reproducible — what resume-equivalence on the GPU needs).
-_BWD_MODE = int(os.environ.get("FT_FLASH_BWD_MODE", "0"))
+# Backward variant: 1 = deterministic (default): KV-major dK/dV kernel + Q-major dQ
+# kernel, no atomics, bit-reproducible — GPU resume is bit-exact with it and it runs
+# as fast as 0 = dQ accumulated with fp32 atomics in the KV-major kernel (330 vs 335 us
+# on the Llama-3-8B layer shape, profiles/r1_flash_bench.log).
+_BWD_MODE = int(os.environ.get("FT_FLASH_BWD_MODE", "1"))
 
 
 def set_deterministic(flag: bool) -> None:

@@ -128,10 +128,9 @@ def train(args) -> int:
     if device.type == "cuda" and model_dtype != torch.bfloat16:
         raise ValueError("the gfx950 kernels are bf16; use --model-dtype bf16 on the GPU (any dtype on --device cpu)")
     torch.manual_seed(args.seed)
-    if args.deterministic:
-        from .ops.attention import set_deterministic
+    from .ops.attention import set_deterministic
 
-        set_deterministic(True)
+    set_deterministic(args.flash_bwd == "deterministic")
     job_id = jobid()
 
     checkpoint = None

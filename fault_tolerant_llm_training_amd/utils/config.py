@@ -169,9 +169,11 @@ def build_parser() -> argparse.ArgumentParser:
         help="Agree on pending stop signals across ranks every N steps",
     )
     parser.add_argument(
-        "--deterministic",
-        action="store_true",
-        help="Bit-reproducible GPU kernels (atomic-free flash-attention dQ); resume is then bit-exact",
+        "--flash-bwd",
+        type=str,
+        default="deterministic",
+        choices=["deterministic", "atomic"],
+        help="Flash-attention backward: atomic-free dQ kernel (bit-reproducible, default) or fp32 atomics",
     )
     parser.add_argument(
         "--profile-steps",

@@ -1,5 +1,10 @@
 """Flash attention fwd / bwd timing on the Llama-3-8B layer shape (B=1, S=2048, 32/8 heads, d=128)."""
+import os
+import sys
+
 import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from fault_tolerant_llm_training_amd._native import kernels
 
@@ -9,7 +14,7 @@ qkv = torch.randn(S, (Hq + 2 * Hkv) * D, device="cuda").bfloat16()
 qk = torch.randn(S, (Hq + Hkv) * D, device="cuda").bfloat16()
 do = torch.randn(S, Hq * D, device="cuda").bfloat16()
 o, lse = K.flash_fwd(qk, qkv, S, Hq, Hkv, D)
-unit = 2 * S * S / 2 * D * 2 * Hq  # one causal matmul, flops
+unit = 2 * (S * S / 2) * D * Hq  # flops of one causal [S x S/2 x D] matmul over all heads
 
 
 def t(fn, it=20):
