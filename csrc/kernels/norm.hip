@@ -19,8 +19,15 @@ namespace {
 
 constexpr int ROWS_PER_BLOCK = 4;  // 4 waves x 64 lanes
 
-template <int CH, bool LN>
+// With ADD: the residual add of the previous sub-block is fused in —
+// h1 = bf16(x + d) is written to `hout` (the residual stream) and normalised, so
+// the projection GEMMs never need a C input (hipBLASLt copies C into a fresh
+// output first) and h1 is read once. Same rounding as the unfused
+// `x = x + f(x)` (bf16 add) followed by the norm.
+template <int CH, bool LN, bool ADD>
 __global__ __launch_bounds__(256) void norm_fwd_kernel(const bf16_t* __restrict__ x,
+                                                       const bf16_t* __restrict__ d,
+                                                       bf16_t* __restrict__ hout,
                                                        const bf16_t* __restrict__ w,
                                                        bf16_t* __restrict__ y,
                                                        float* __restrict__ rstd,
@@ -38,6 +45,13 @@ __global__ __launch_bounds__(256) void norm_fwd_kernel(const bf16_t* __restrict_
     if (idx < N) {
       uint4 raw = *reinterpret_cast<const uint4*>(xr + idx);
       unpack8(raw, v[c]);
+      if constexpr (ADD) {
+        float dv[8];
+        unpack8(*reinterpret_cast<const uint4*>(d + (size_t)row * N + idx), dv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[c][j] = bf2f(f2bf(v[c][j] + dv[j]));
+        *reinterpret_cast<uint4*>(hout + (size_t)row * N + idx) = pack8(v[c]);
+      }
     } else {
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[c][j] = 0.f;
@@ -216,14 +230,14 @@ __global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ p
   }
 }
 
-template <bool LN>
-void launch_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, float* rstd, float* mean, int M,
-                int N, float eps, hipStream_t st) {
+template <bool LN, bool ADD>
+void launch_fwd(const bf16_t* x, const bf16_t* d, bf16_t* hout, const bf16_t* w, bf16_t* y,
+                float* rstd, float* mean, int M, int N, float eps, hipStream_t st) {
   const int chunks = (N + 511) / 512;
   dim3 grid((M + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK), block(256);
-#define FT_NF(C)                                                                              \
-  hipLaunchKernelGGL((norm_fwd_kernel<C, LN>), grid, block, 0, st, x, w, y, rstd, mean, M, N, \
-                     eps)
+#define FT_NF(C)                                                                             \
+  hipLaunchKernelGGL((norm_fwd_kernel<C, LN, ADD>), grid, block, 0, st, x, d, hout, w, y, rstd, \
+                     mean, M, N, eps)
   if (chunks <= 1) FT_NF(1);
   else if (chunks <= 2) FT_NF(2);
   else if (chunks <= 4) FT_NF(4);
@@ -254,9 +268,11 @@ void launch_bwd(const bf16_t* dy, const bf16_t* x, const bf16_t* w, const float*
 
 }  // namespace
 
-// Returns (y, rstd, mean). `mean` is empty for RMSNorm.
-std::tuple<at::Tensor, at::Tensor, at::Tensor> norm_fwd(const at::Tensor& x, const at::Tensor& w,
-                                                       double eps, bool layernorm) {
+// Returns (y, rstd, mean, h). `mean` is empty for RMSNorm. With `d` given, the input
+// is h = bf16(x + d) (fused residual add) and h is returned; otherwise h is empty.
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> add_norm_fwd(
+    const at::Tensor& x, const std::optional<at::Tensor>& d, const at::Tensor& w, double eps,
+    bool layernorm) {
   FT_CHECK_CUDA(x);
   FT_CHECK_BF16(x);
   FT_CHECK_BF16(w);
@@ -266,19 +282,33 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> norm_fwd(const at::Tensor& x, con
   TORCH_CHECK(w.numel() == N, "norm: weight size mismatch");
   TORCH_CHECK(N % 8 == 0, "norm: N must be a multiple of 8");
   const int M = x.numel() / N;
+  const bool add = d.has_value() && d->defined();
+  if (add) {
+    FT_CHECK_BF16((*d));
+    FT_CHECK_CONTIG((*d));
+    TORCH_CHECK(d->numel() == x.numel(), "add_norm: residual delta shape mismatch");
+  }
   const at::DeviceGuard guard(x.device());
   auto y = at::empty_like(x);
   auto rstd = at::empty({M}, x.options().dtype(at::kFloat));
   at::Tensor mean = at::empty({layernorm ? M : 0}, x.options().dtype(at::kFloat));
-  if (M == 0) return {y, rstd, mean};
-  if (layernorm)
-    launch_fwd<true>(cptr<bf16_t>(x), cptr<bf16_t>(w), mptr<bf16_t>(y), mptr<float>(rstd),
-                     mptr<float>(mean), M, N, (float)eps, ft_stream());
-  else
-    launch_fwd<false>(cptr<bf16_t>(x), cptr<bf16_t>(w), mptr<bf16_t>(y), mptr<float>(rstd),
-                      nullptr, M, N, (float)eps, ft_stream());
+  at::Tensor h = add ? at::empty_like(x) : at::empty({0}, x.options());
+  if (M == 0) return {y, rstd, mean, h};
+  const bf16_t* dp = add ? cptr<bf16_t>(*d) : nullptr;
+  bf16_t* hp = add ? mptr<bf16_t>(h) : nullptr;
+  float* mp = layernorm ? mptr<float>(mean) : nullptr;
+  if (layernorm && add) launch_fwd<true, true>(cptr<bf16_t>(x), dp, hp, cptr<bf16_t>(w), mptr<bf16_t>(y), mptr<float>(rstd), mp, M, N, (float)eps, ft_stream());
+  else if (layernorm) launch_fwd<true, false>(cptr<bf16_t>(x), dp, hp, cptr<bf16_t>(w), mptr<bf16_t>(y), mptr<float>(rstd), mp, M, N, (float)eps, ft_stream());
+  else if (add) launch_fwd<false, true>(cptr<bf16_t>(x), dp, hp, cptr<bf16_t>(w), mptr<bf16_t>(y), mptr<float>(rstd), mp, M, N, (float)eps, ft_stream());
+  else launch_fwd<false, false>(cptr<bf16_t>(x), dp, hp, cptr<bf16_t>(w), mptr<bf16_t>(y), mptr<float>(rstd), mp, M, N, (float)eps, ft_stream());
   FT_LAUNCH_CHECK();
-  return {y, rstd, mean};
+  return {y, rstd, mean, h};
+}
+
+std::tuple<at::Tensor, at::Tensor, at::Tensor> norm_fwd(const at::Tensor& x, const at::Tensor& w,
+                                                       double eps, bool layernorm) {
+  auto r = add_norm_fwd(x, std::nullopt, w, eps, layernorm);
+  return {std::get<0>(r), std::get<1>(r), std::get<2>(r)};
 }
 
 // Returns dx; writes (or accumulates) dw into `dw` (a view into the flat grad buffer).
@@ -328,6 +358,10 @@ at::Tensor norm_bwd(const at::Tensor& dy, const at::Tensor& x, const at::Tensor&
 TORCH_LIBRARY_FRAGMENT(ftamd, m) {
   m.def("norm_fwd(Tensor x, Tensor w, float eps, bool layernorm) -> (Tensor, Tensor, Tensor)",
         &norm_fwd);
+  m.def(
+      "add_norm_fwd(Tensor x, Tensor? d, Tensor w, float eps, bool layernorm) -> (Tensor, Tensor, "
+      "Tensor, Tensor)",
+      &add_norm_fwd);
   m.def(
       "norm_bwd(Tensor dy, Tensor x, Tensor w, Tensor rstd, Tensor? mean, Tensor(a!) dw, "
       "Tensor? dres, bool accumulate) -> Tensor",

@@ -130,17 +130,24 @@ class TransformerBlock(nn.Module):
         self.eps = a.norm_eps
         self.layernorm = a.norm_type == "layernorm"
 
-    def forward(self, x, cos, sin, seq_len):
+    def forward(self, h, d, cos, sin, seq_len):
+        """Pre-norm block (reference model.py:310-311) on the residual stream ``h`` with the
+        previous block's pending output ``d`` (its add is fused into this block's first norm).
+        Returns (h', d') with the block output h' + d' still to be added."""
         at, ff = self.attention, self.feed_forward
         sk = lambda p: getattr(p, "_ft_sink", None)  # noqa: E731
-        xn = Fx.norm(x, self.attention_norm.weight, sk(self.attention_norm.weight), self.eps, self.layernorm)
+        if d is None:
+            xn = Fx.norm(h, self.attention_norm.weight, sk(self.attention_norm.weight), self.eps, self.layernorm)
+        else:
+            h, xn = Fx.add_norm(h, d, self.attention_norm.weight, sk(self.attention_norm.weight), self.eps,
+                                self.layernorm)
         qkv = Fx.linear(xn, at.wqkv, at.wqkv_sink)
         o = Fx.rope_attention(qkv.view(-1, qkv.shape[-1]), cos, sin, seq_len, at.n_heads, at.n_kv_heads, at.head_dim)
-        x = Fx.linear(o.view(*x.shape[:-1], -1), at.wo.weight, sk(at.wo.weight), residual=x)
-        hn = Fx.norm(x, self.ffn_norm.weight, sk(self.ffn_norm.weight), self.eps, self.layernorm)
+        da = Fx.linear(o.view(*h.shape[:-1], -1), at.wo.weight, sk(at.wo.weight))
+        h, hn = Fx.add_norm(h, da, self.ffn_norm.weight, sk(self.ffn_norm.weight), self.eps, self.layernorm)
         gu = Fx.linear(hn, ff.w13, ff.w13_sink)
         a = Fx.swiglu(gu)
-        return Fx.linear(a, ff.w2.weight, sk(ff.w2.weight), residual=x)
+        return h, Fx.linear(a, ff.w2.weight, sk(ff.w2.weight))
 
 
 class Transformer(nn.Module):
@@ -244,12 +251,17 @@ class Transformer(nn.Module):
         self._wait(emb_r)
         h = Fx.embedding(tokens, self.tok_embeddings.weight, sk(self.tok_embeddings.weight))
         cos, sin = self.rope_cos, self.rope_sin
+        d = None
         for i, layer in enumerate(self.layers.values()):
             self._wait(layer_r[i])
-            h = layer(h, cos, sin, S)
+            h, d = layer(h, d, cos, sin, S)
         self._wait(final_r)
         a = self.model_args
-        h = Fx.norm(h, self.norm.weight, sk(self.norm.weight), a.norm_eps, a.norm_type == "layernorm")
+        ln = a.norm_type == "layernorm"
+        if d is None:
+            h = Fx.norm(h, self.norm.weight, sk(self.norm.weight), a.norm_eps, ln)
+        else:
+            _, h = Fx.add_norm(h, d, self.norm.weight, sk(self.norm.weight), a.norm_eps, ln)
         if labels is None:
             return Fx.linear(h, self.output.weight, sk(self.output.weight))
         if inv_count is None:

@@ -155,6 +155,53 @@ def norm(x, weight, sink=None, eps: float = 1e-5, layernorm: bool = False):
     return NormFn.apply(x, weight, sink, eps, layernorm)
 
 
+class AddNormFn(torch.autograd.Function):
+    """(h, y) = (x + d, norm(x + d)): the residual add of the previous sub-block fused
+    into the next pre-norm (reference model.py:310-311 ``h = x + attn(norm(x))``).
+
+    Backward is one kernel: dh_total = dres + norm_bwd(dy), returned for both x and d.
+    """
+
+    @staticmethod
+    def forward(ctx, x, d, weight, sink, eps, layernorm):
+        ctx.sink, ctx.eps, ctx.ln = sink, eps, layernorm
+        if x.is_cuda:
+            y, rstd, mean, h = kernels().add_norm_fwd(x.contiguous(), d.contiguous(), weight, eps, layernorm)
+            ctx.save_for_backward(h, weight, rstd, mean)
+            return h, y
+        h = x + d
+        ctx.save_for_backward(h, weight)
+        return h, norm_reference(h, weight, eps, layernorm)
+
+    @staticmethod
+    def backward(ctx, dh, dy):
+        sink = ctx.sink
+        if dy.is_cuda:
+            h, w, rstd, mean = ctx.saved_tensors
+            dres = dh.contiguous() if dh is not None else None
+            buf = sink.buf if sink is not None else torch.empty_like(w)
+            g = kernels().norm_bwd(dy.contiguous(), h, w, rstd, mean, buf, dres,
+                                   sink.accumulate if sink is not None else False)
+            if sink is not None:
+                sink.ready()
+                return g, g, None, None, None, None
+            return g, g, buf, None, None, None
+        h, w = ctx.saved_tensors
+        with torch.enable_grad():
+            hr = h.detach().requires_grad_(True)
+            wr = w.detach().requires_grad_(True)
+            y = norm_reference(hr, wr, ctx.eps, ctx.ln)
+            g, dw = torch.autograd.grad(y, (hr, wr), dy)
+        if dh is not None:
+            g = g + dh
+        return g, g, _write_weight_grad(sink, dw), None, None, None
+
+
+def add_norm(x, d, weight, sink=None, eps: float = 1e-5, layernorm: bool = False):
+    """Returns (x + d, norm(x + d))."""
+    return AddNormFn.apply(x, d, weight, sink, eps, layernorm)
+
+
 # --------------------------------------------------------------------------------------
 # Linear (+ fused residual add through the GEMM's C input)
 # --------------------------------------------------------------------------------------

@@ -1,0 +1,9 @@
+#!/bin/bash
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+S=scripts/gpu_check.sh
+$S pytest_gpu 500 python -m pytest tests -m gpu -x -q || exit 1
+$S b_addnorm 300 python bench.py --steps 10 --warmup 3 || exit 1
+$S flash_bench 300 python scripts/flash_bench.py || exit 1
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+$S prof5 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof5 -o run --output-format csv -- python3 bench.py --steps 3 --warmup 2 || exit 1

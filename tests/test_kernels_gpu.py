@@ -213,3 +213,28 @@ def test_weight_grad_layouts(mode, monkeypatch):
     dw = Fx.weight_grad(dy, x, None)
     ref = dy.float().t() @ x.float()
     assert rel(dw, ref) < 1e-2
+
+
+@pytest.mark.parametrize("ln", [False, True])
+def test_add_norm_fused(ln):
+    """AddNormFn on the GPU (fused residual add + norm, norm bwd with the residual grad fused)
+    vs fp32 autograd of h = x + d, y = norm(h)."""
+    from fault_tolerant_llm_training_amd.ops.functional import add_norm
+
+    torch.manual_seed(3)
+    M, N = 300, 4096
+    x = torch.randn(M, N, device="cuda").bfloat16().requires_grad_(True)
+    d = torch.randn(M, N, device="cuda").bfloat16().requires_grad_(True)
+    w = (1 + 0.1 * torch.randn(N, device="cuda")).bfloat16().requires_grad_(True)
+    h, y = add_norm(x, d, w, None, 1e-5, ln)
+    dh = torch.randn(M, N, device="cuda").bfloat16()
+    dy = torch.randn(M, N, device="cuda").bfloat16()
+    torch.autograd.backward((h, y), (dh, dy))
+    xr, dr, wr = (t.detach().float().requires_grad_(True) for t in (x, d, w))
+    hr = xr + dr
+    hc = hr - hr.mean(-1, keepdim=True) if ln else hr
+    yr = hc * torch.rsqrt(hc.pow(2).mean(-1, keepdim=True) + 1e-5) * wr
+    torch.autograd.backward((hr, yr), (dh.float(), dy.float()))
+    assert rel(h, hr) < 1e-2 and rel(y, yr) < 1e-2
+    assert rel(x.grad, xr.grad) < 2e-2 and torch.equal(x.grad, d.grad)
+    assert rel(w.grad, wr.grad) < 2e-2
