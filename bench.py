@@ -59,6 +59,10 @@ def main():
 
     info = fdist.init_distributed(a.device)
     dev = info.device
+    if os.environ.get("FT_COMPUTE_PRIORITY") == "1":
+        # compute on a high-priority stream: its workgroups are dispatched ahead of the
+        # optimizer/snapshot side streams when both have work queued
+        torch.cuda.set_stream(torch.cuda.Stream(device=dev, priority=-1))
     world = info.world_size
     if a.gpus != world and info.is_main:
         print(f"[bench] note: --gpus {a.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)

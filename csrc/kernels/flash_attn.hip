@@ -161,7 +161,15 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(const bf16_t* __restr
   const int nqt = (S + BM - 1) / BM;
   const int per = B * Hq;
   const int L = blockIdx.x;
-  const int qt = nqt - 1 - L / per;  // heaviest causal tiles first
+  // Causal work of q-tile qt is ∝ qt+1. With 2 resident blocks per CU, block L and
+  // block L + grid/2 share a CU: the first half runs the heavy tiles heaviest-first,
+  // the second half the light tiles lightest-first, so each CU's pair sums to the
+  // same work (nqt+1 tiles) instead of heavy+heavy next to light+light.
+  int qt;
+  if ((nqt & 1) == 0 && L >= (nqt / 2) * per)
+    qt = (L - (nqt / 2) * per) / per;
+  else
+    qt = nqt - 1 - L / per;
   const int rem = L % per;
   const int b = rem / Hq;
   int h, kvh;

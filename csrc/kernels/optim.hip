@@ -169,7 +169,10 @@ void adamw_(const at::Tensor& p, const at::Tensor& g, const at::Tensor& m, const
   const float bc2 = 1.f - (float)std::pow(beta2, (double)step);
   const float inv_bc1 = 1.f / bc1, inv_sqrt_bc2 = 1.f / std::sqrt(bc2);
   int nb = stream_grid(n8);
-  if (max_blocks > 0) nb = std::max(1, std::min(nb, (int)max_blocks));
+  // max_blocks > 0 overrides the default grid cap (both directions): small grids
+  // leave CUs to a concurrent stream, large ones make every block short-lived so
+  // the dispatcher can interleave a higher-priority stream's workgroups.
+  if (max_blocks > 0) nb = (int)std::max(1L, std::min((n8 + 255) / 256, (long)max_blocks));
   const dim3 grid(nb), block(256);
 #define FT_ADAM(PT, ST)                                                                            \
   hipLaunchKernelGGL((adamw_kernel<PT, ST>), grid, block, 0, ft_stream(), mptr<PT>(p), cptr<PT>(g), \
