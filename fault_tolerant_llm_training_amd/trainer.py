@@ -60,32 +60,57 @@ class InjectedFault(Exception):
 
 
 class _LossLog:
-    """Deferred loss logging: D2H of the scalar into pinned memory + an event,
-    printed at a later step boundary once the copy has landed (no host stall)."""
+    """Deferred step logging without host stalls.
 
-    def __init__(self, device: torch.device):
+    At a log step the loss is copied D2H into pinned memory and a timing event is
+    recorded on the compute stream; the line is printed at a later step boundary
+    once the event has completed. Step time is the GPU time between consecutive
+    log events (the host runs ahead of the GPU, so host timestamps would measure
+    enqueue time, not step time).
+    """
+
+    def __init__(self, device: torch.device, tokens_per_step: int, world: int, flops_per_token: float):
         self.cuda = device.type == "cuda"
-        self.pending = []  # (step, host tensor, event, extra)
+        self.pending = []  # (step, host loss, event, extra)
+        self.tokens = tokens_per_step
+        self.world = world
+        self.fpt = flops_per_token
+        self.last = None  # (step, event or host time)
+
+    def mark(self):
+        """Timing origin (call once the first step is enqueued)."""
+        self.last = None
 
     def push(self, step: int, loss: torch.Tensor, extra: Dict[str, Any]):
         if self.cuda:
             h = torch.empty(1, dtype=torch.float32, pin_memory=True)
             h.copy_(loss.detach().float().reshape(1), non_blocking=True)
-            ev = torch.cuda.Event()
+            ev = torch.cuda.Event(enable_timing=True)
             ev.record()
             self.pending.append((step, h, ev, extra))
         else:
-            self.pending.append((step, loss.detach().float().reshape(1), None, extra))
+            self.pending.append((step, loss.detach().float().reshape(1), time.perf_counter(), extra))
 
     def flush(self, force: bool = False):
         keep = []
         for step, h, ev, extra in self.pending:
-            if ev is not None and not force and not ev.query():
+            if self.cuda and not force and not ev.query():
                 keep.append((step, h, ev, extra))
                 continue
-            if ev is not None:
+            if self.cuda:
                 ev.synchronize()
             msg = f"Training step: {step} | Loss: {h.item():.2f}"
+            if self.last is not None:
+                ls, lev = self.last
+                dt = (lev.elapsed_time(ev) / 1e3) if self.cuda else (ev - lev)
+                dt /= max(1, step - ls)
+                tok_s = self.tokens / dt
+                extra = dict(extra)
+                extra["step_ms"] = f"{dt * 1e3:.1f}"
+                extra["tok/s"] = f"{tok_s:.0f}"
+                if self.cuda:
+                    extra["MFU"] = f"{tok_s / self.world * self.fpt / 2.5e15:.3f}"
+            self.last = (step, ev)
             if extra:
                 msg += " | " + " | ".join(f"{k}: {v}" for k, v in extra.items())
             logger.info(msg)
@@ -256,7 +281,7 @@ def train(args) -> int:
     metrics_f = open(args.metrics_file, "a") if (args.metrics_file and info.is_main) else None
     B, S, W = args.batch_size, args.sequence_length, info.world_size
     fpt = flops_per_token(margs, S)
-    losslog = _LossLog(device)
+    losslog = _LossLog(device, B * S * W, W, fpt)
     synthetic_counts = args.synthetic_data  # no ignore_index labels: the global count is static
     inv_static = None
     if synthetic_counts:
@@ -301,19 +326,16 @@ def train(args) -> int:
             steps_window += 1
 
             if training_step == 1 or training_step % args.logging_frequency == 0:
-                now = time.perf_counter()
-                dt = (now - t_window) / max(1, steps_window)
-                tok_s = B * S * W / dt
-                extra = {"step_ms": f"{dt * 1e3:.1f}", "tok/s": f"{tok_s:.0f}",
-                         "MFU": f"{tok_s / W * fpt / 2.5e15:.3f}" if device.type == "cuda" else "n/a",
-                         "lr": f"{lr_now:.3e}"}
+                extra = {"lr": f"{lr_now:.3e}"}
                 if device.type == "cuda":
                     extra["peak_HBM_GB"] = f"{torch.cuda.max_memory_allocated(device) / 2**30:.1f}"
                 losslog.push(training_step, loss, extra)
                 if metrics_f is not None:
-                    metrics_f.write(json.dumps({"step": training_step, "step_ms": dt * 1e3, "tok_s": tok_s}) + "\n")
+                    now = time.perf_counter()
+                    dt = (now - t_window) / max(1, steps_window)
+                    metrics_f.write(json.dumps({"step": training_step, "host_step_ms": dt * 1e3}) + "\n")
                     metrics_f.flush()
-                t_window, steps_window = now, 0
+                    t_window, steps_window = now, 0
             training_step += 1
             if prof is not None and training_step >= prof_range[1]:
                 if device.type == "cuda":
