@@ -7,7 +7,10 @@ seq 2048, batch 1 per GPU, bf16 params/grads/AdamW states, lr 5e-5 with 100
 warmup steps, grad clipping at 1.0 — the reference's logged run (train.sh:16-20).
 Synthetic tokens, random-init weights (no network on the GPU box). Every timed
 step is a full training step: H2D of the batch, forward, backward with the
-bucketed RCCL all-reduce, gradient norm + clip, AdamW, LR-scheduler step.
+gradient buckets' RCCL collectives launched as backward produces them (ZeRO-1
+reduce-scatter by default for N > 1; ``--dp-mode allreduce`` for replicated
+state), gradient norm + clip, AdamW (+ parameter all-gather under ZeRO-1),
+LR-scheduler step.
 
     python bench.py --gpus N --steps K --warmup W
     torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU)
@@ -48,6 +51,11 @@ def parse():
     return ap.parse_args()
 
 
+def _sync(dev):
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+
+
 def main():
     a = parse()
     from fault_tolerant_llm_training_amd.parallel import dist as fdist
@@ -59,7 +67,7 @@ def main():
 
     info = fdist.init_distributed(a.device)
     dev = info.device
-    if os.environ.get("FT_COMPUTE_PRIORITY") == "1":
+    if os.environ.get("FT_COMPUTE_PRIORITY") == "1" and dev.type == "cuda":
         # compute on a high-priority stream: its workgroups are dispatched ahead of the
         # optimizer/snapshot side streams when both have work queued
         torch.cuda.set_stream(torch.cuda.Stream(device=dev, priority=-1))
@@ -99,16 +107,16 @@ def main():
 
     for i in range(a.warmup):
         loss = step(i)
-    torch.cuda.synchronize()
+    _sync(dev)
     fdist.barrier()
-    torch.cuda.synchronize()
+    _sync(dev)
     t0 = time.perf_counter()
     for i in range(a.steps):
         loss = step(a.warmup + i)
     opt.gate.wait_all()
-    torch.cuda.synchronize()
+    _sync(dev)
     fdist.barrier()
-    torch.cuda.synchronize()
+    _sync(dev)
     elapsed = time.perf_counter() - t0
     elapsed = fdist.ctrl_allreduce_max(int(elapsed * 1e9)) / 1e9
     final_loss = float(loss.item())

@@ -67,6 +67,9 @@ def init_distributed(device_type: str = "cuda", timeout_s: int = 1800) -> DistIn
         os.environ.setdefault("MASTER_PORT", "29500")
         os.environ["RANK"], os.environ["WORLD_SIZE"] = str(rank), str(world)
         timeout = datetime.timedelta(seconds=timeout_s)
+        # RCCL kernels on a high-priority stream: the bucket collectives that overlap
+        # backward / the next forward get CU slots ahead of queued GEMM workgroups
+        os.environ.setdefault("TORCH_NCCL_HIGH_PRIORITY", "1")
         if not dist.is_initialized():
             if device_type == "cuda":
                 dist.init_process_group("nccl", timeout=timeout, device_id=device)

@@ -1,0 +1,68 @@
+"""bench.py driver contract (single JSON line, whole-job value, max over ranks) on CPU/gloo.
+
+The driver runs ``python bench.py`` for N=1 and ``torch.distributed.run ... bench.py --gpus N``
+for N>1; this exercises the same code path (process groups, gradient reducer modes, barriers,
+max-over-ranks timing) with gloo and a tiny model.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+from helpers import ROOT
+
+pytestmark = pytest.mark.slow
+
+ARGS = ["--device", "cpu", "--model", "tiny", "--vocab-size", "256", "--seq-len", "64", "--steps", "2",
+        "--warmup", "1", "--bucket-mb", "0.1"]
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _env():
+    env = dict(os.environ)
+    env["OMP_NUM_THREADS"] = "1"
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+        env.pop(k, None)
+    return env
+
+
+def _json_lines(out):
+    return [json.loads(ln) for ln in out.splitlines() if ln.startswith("{")]
+
+
+def test_bench_single_process_json():
+    r = subprocess.run([sys.executable, "bench.py"] + ARGS, cwd=ROOT, env=_env(), capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1
+    j = lines[0]
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config"):
+        assert k in j, k
+    assert j["n_gpus"] == 1 and j["steps"] == 2 and j["config"]["parallelism"] == "dp1"
+    assert abs(j["value"] - 64 / (j["ms_per_step"] / 1e3)) / j["value"] < 0.02
+
+
+@pytest.mark.parametrize("mode", ["zero1", "allreduce"])
+def test_bench_torchrun_two_ranks(mode):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2", "--dp-mode", mode] + ARGS
+    r = subprocess.run(cmd, cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1, r.stdout  # rank 0 only
+    j = lines[0]
+    assert j["n_gpus"] == 2 and j["config"]["parallelism"] == "dp2" and j["config"]["global_batch"] == 2
+    assert j["grad_mode"] == mode
+    assert abs(j["value"] - 2 * 64 / (j["ms_per_step"] / 1e3)) / j["value"] < 0.02
