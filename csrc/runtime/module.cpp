@@ -44,6 +44,10 @@ PYBIND11_MODULE(_runtime, m) {
       .def("add_bytes",
            [](ZipWriter& w, const std::string& name, py::bytes b) { w.add_bytes(name, std::string(b)); })
       .def("add_buffer", &ZipWriter::add_buffer)
+      .def("add_external", &ZipWriter::add_external)
+      .def("set_external_crc", &ZipWriter::set_external_crc)
+      .def("layout_records", &ZipWriter::layout_records)
+      .def("create_file", &ZipWriter::create_file)
       .def("total_size", &ZipWriter::total_size)
       .def("start", &ZipWriter::start, py::arg("wait_event") = 0, py::arg("fsync") = true)
       .def("run_sync", &ZipWriter::run_sync, py::arg("wait_event") = 0, py::arg("fsync") = true,
@@ -62,5 +66,10 @@ PYBIND11_MODULE(_runtime, m) {
       .def("event_handle", &SnapshotEngine::event_handle)
       .def("stream_handle", &SnapshotEngine::stream_handle);
 
+  m.def("write_pieces", &write_pieces, py::arg("path"), py::arg("file_offs"), py::arg("ptrs"), py::arg("lens"),
+        py::arg("nthreads") = 8, py::arg("wait_event") = 0, py::arg("fsync") = true, py::arg("direct") = true,
+        py::call_guard<py::gil_scoped_release>(),
+        "Sharded save: CRC + pwrite this rank's pieces into an existing file; returns per-piece CRC32s");
+  m.def("crc32_combine", &crc32_combine_u32);
   m.def("pinned_empty", &pinned_empty, "Exact-size pinned host buffer (hipHostMalloc) as a uint8 tensor");
 }

@@ -9,6 +9,7 @@
 #include <stdexcept>
 #include <string>
 #include <thread>
+#include <tuple>
 #include <vector>
 
 namespace ftrt {
@@ -39,7 +40,26 @@ struct ZipRecord {
   uint16_t extra_len = 0;
   bool zip64 = false;
   uint32_t crc = 0;
+  bool external = false;   // bytes written by other processes (sharded save); crc given
 };
+
+// One contiguous piece of a file: `len` bytes from host `ptr` to file offset `file_off`.
+struct FilePiece {
+  uint64_t file_off = 0;
+  const uint8_t* ptr = nullptr;
+  uint64_t len = 0;
+  uint32_t crc = 0;
+};
+
+// Parallel CRC32 + pwrite of pieces (O_DIRECT for 4 KiB-aligned bodies when dfd >= 0).
+// Fills each piece's crc; returns bytes written with O_DIRECT.
+uint64_t write_pieces_fd(int fd, int dfd, std::vector<FilePiece>& pieces, int nthreads, uint64_t chunk);
+
+// Sharded-save helpers (every rank writes its own pieces of one shared file).
+std::vector<uint32_t> write_pieces(const std::string& path, const std::vector<uint64_t>& file_offs,
+                                   const std::vector<uint64_t>& ptrs, const std::vector<uint64_t>& lens,
+                                   int nthreads, uintptr_t wait_event, bool do_fsync, bool direct);
+uint32_t crc32_combine_u32(uint32_t crc1, uint32_t crc2, uint64_t len2);
 
 struct ZipStats {
   double seconds = 0, write_seconds = 0, fsync_seconds = 0, wait_seconds = 0;
@@ -55,6 +75,14 @@ class ZipWriter {
   ~ZipWriter();
   void add_bytes(const std::string& name, const std::string& bytes);
   void add_buffer(const std::string& name, uintptr_t ptr, uint64_t nbytes);
+  // A record whose bytes other processes write into the same file (sharded save).
+  void add_external(const std::string& name, uint64_t nbytes, uint32_t crc);
+  void set_external_crc(const std::string& name, uint32_t crc);
+  // (name, data offset, size) of every record after layout.
+  std::vector<std::tuple<std::string, uint64_t, uint64_t>> layout_records();
+  // Create the temp file sized to the data region so other ranks can pwrite into it;
+  // the final run() then does not truncate it.
+  void create_file();
   // Spawn the writer thread. If wait_event != 0 it is a hipEvent_t that must
   // complete before host memory is read (the D2H snapshot).
   void start(uintptr_t wait_event, bool do_fsync);
@@ -74,6 +102,7 @@ class ZipWriter {
   bool laid_out_ = false;
   bool direct_ = true;       // align big records and try O_DIRECT
   bool direct_used_ = true;
+  bool truncate_ = true;
   std::thread th_;
   std::atomic<bool> done_{false};
   ZipStats stats_;

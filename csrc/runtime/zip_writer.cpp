@@ -86,6 +86,119 @@ std::string dirname_of(const std::string& p) {
 
 }  // namespace
 
+uint64_t write_pieces_fd(int fd, int dfd, std::vector<FilePiece>& pieces, int nthreads, uint64_t chunk) {
+  // split into <= chunk work items so the pool stays balanced
+  struct Item {
+    size_t piece;
+    uint64_t off, len;
+    uint32_t crc;
+  };
+  std::vector<Item> items;
+  for (size_t i = 0; i < pieces.size(); ++i) {
+    if (pieces[i].len == 0) items.push_back({i, 0, 0, 0});
+    for (uint64_t o = 0; o < pieces[i].len; o += chunk) items.push_back({i, o, std::min(chunk, pieces[i].len - o), 0});
+  }
+  std::atomic<size_t> next{0};
+  std::atomic<uint64_t> direct_bytes{0};
+  std::string err;
+  std::mutex err_mu;
+  auto worker = [&] {
+    for (;;) {
+      size_t k = next.fetch_add(1);
+      if (k >= items.size()) return;
+      Item& c = items[k];
+      const FilePiece& pc = pieces[c.piece];
+      try {
+        const uint8_t* p = pc.ptr + c.off;
+        uLong crc = crc32(0L, Z_NULL, 0);
+        uint64_t done = 0;
+        while (done < c.len) {
+          const uInt n = (uInt)std::min<uint64_t>(c.len - done, 1u << 30);
+          crc = crc32(crc, p + done, n);
+          done += n;
+        }
+        c.crc = (uint32_t)crc;
+        if (c.len) {
+          const uint64_t foff = pc.file_off + c.off;
+          const uint64_t body = (dfd >= 0 && foff % DIRECT_ALIGN == 0 &&
+                                 reinterpret_cast<uintptr_t>(p) % DIRECT_ALIGN == 0)
+                                    ? c.len / DIRECT_ALIGN * DIRECT_ALIGN
+                                    : 0;
+          if (body) {
+            if (!pwrite_direct(dfd, p, body, foff)) {
+              pwrite_all(fd, p, body, foff);  // O_DIRECT refused at write time
+            } else {
+              direct_bytes.fetch_add(body);
+            }
+          }
+          if (c.len > body) pwrite_all(fd, p + body, c.len - body, foff + body);
+        }
+      } catch (const std::exception& ex) {
+        std::lock_guard<std::mutex> g(err_mu);
+        err = ex.what();
+        next.store(items.size());
+      }
+    }
+  };
+  std::vector<std::thread> pool;
+  const int nt = (int)std::min<size_t>(nthreads < 1 ? 1 : nthreads, std::max<size_t>(1, items.size()));
+  for (int t = 0; t < nt; ++t) pool.emplace_back(worker);
+  for (auto& t : pool) t.join();
+  if (!err.empty()) throw std::runtime_error(err);
+  // fold the item CRCs into per-piece CRCs (in order)
+  std::vector<bool> first(pieces.size(), true);
+  for (const auto& c : items) {
+    auto& pc = pieces[c.piece];
+    if (first[c.piece]) {
+      pc.crc = c.crc;
+      first[c.piece] = false;
+    } else {
+      pc.crc = (uint32_t)crc32_combine64(pc.crc, c.crc, (z_off64_t)c.len);
+    }
+  }
+  return direct_bytes.load();
+}
+
+std::vector<uint32_t> write_pieces(const std::string& path, const std::vector<uint64_t>& file_offs,
+                                   const std::vector<uint64_t>& ptrs, const std::vector<uint64_t>& lens,
+                                   int nthreads, uintptr_t wait_event, bool do_fsync, bool direct) {
+  if (file_offs.size() != ptrs.size() || ptrs.size() != lens.size())
+    throw std::runtime_error("write_pieces: length mismatch");
+  if (wait_event) {
+    hipError_t e = hipEventSynchronize(reinterpret_cast<hipEvent_t>(wait_event));
+    if (e != hipSuccess) throw std::runtime_error(std::string("hipEventSynchronize: ") + hipGetErrorString(e));
+  }
+  std::vector<FilePiece> pieces(file_offs.size());
+  for (size_t i = 0; i < pieces.size(); ++i) {
+    pieces[i].file_off = file_offs[i];
+    pieces[i].ptr = reinterpret_cast<const uint8_t*>(ptrs[i]);
+    pieces[i].len = lens[i];
+  }
+  int fd = ::open(path.c_str(), O_WRONLY | O_CLOEXEC);
+  if (fd < 0) throw std::runtime_error("open(" + path + "): " + strerror(errno));
+  int dfd = direct ? ::open(path.c_str(), O_WRONLY | O_DIRECT | O_CLOEXEC) : -1;
+  std::string err;
+  try {
+    write_pieces_fd(fd, dfd, pieces, nthreads, 64ull << 20);
+  } catch (const std::exception& ex) {
+    err = ex.what();
+  }
+  if (dfd >= 0) {
+    if (do_fsync) ::fdatasync(dfd);
+    ::close(dfd);
+  }
+  if (do_fsync) ::fdatasync(fd);
+  ::close(fd);
+  if (!err.empty()) throw std::runtime_error(err);
+  std::vector<uint32_t> crcs;
+  for (const auto& p : pieces) crcs.push_back(p.crc);
+  return crcs;
+}
+
+uint32_t crc32_combine_u32(uint32_t crc1, uint32_t crc2, uint64_t len2) {
+  return (uint32_t)crc32_combine64(crc1, crc2, (z_off64_t)len2);
+}
+
 ZipWriter::ZipWriter(std::string tmp_path, std::string final_path, std::string archive,
                      int nthreads, uint64_t chunk_bytes, bool direct)
     : tmp_(std::move(tmp_path)),
@@ -117,10 +230,50 @@ void ZipWriter::add_buffer(const std::string& name, uintptr_t ptr, uint64_t nbyt
   laid_out_ = false;
 }
 
+void ZipWriter::add_external(const std::string& name, uint64_t nbytes, uint32_t crc) {
+  ZipRecord r;
+  r.name = archive_ + "/" + name;
+  r.size = nbytes;
+  r.crc = crc;
+  r.external = true;
+  recs_.push_back(std::move(r));
+  laid_out_ = false;
+}
+
+void ZipWriter::set_external_crc(const std::string& name, uint32_t crc) {
+  const std::string full = archive_ + "/" + name;
+  for (auto& r : recs_)
+    if (r.name == full && r.external) {
+      r.crc = crc;
+      return;
+    }
+  throw std::runtime_error("set_external_crc: no external record " + name);
+}
+
+std::vector<std::tuple<std::string, uint64_t, uint64_t>> ZipWriter::layout_records() {
+  if (!laid_out_) layout();
+  std::vector<std::tuple<std::string, uint64_t, uint64_t>> out;
+  for (const auto& r : recs_) out.emplace_back(r.name.substr(archive_.size() + 1), r.data_off, r.size);
+  return out;
+}
+
+void ZipWriter::create_file() {
+  if (!laid_out_) layout();
+  int fd = ::open(tmp_.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
+  if (fd < 0) throw std::runtime_error("open(" + tmp_ + "): " + strerror(errno));
+  if (::ftruncate(fd, (off_t)cd_off_) != 0) {
+    ::close(fd);
+    throw std::runtime_error(std::string("ftruncate: ") + strerror(errno));
+  }
+  ::close(fd);
+  truncate_ = false;
+}
+
 void ZipWriter::layout() {
   uint64_t off = 0;
   for (auto& r : recs_) {
-    if (!r.owned.empty() || r.data == nullptr) r.data = reinterpret_cast<const uint8_t*>(r.owned.data());
+    if (!r.external && (!r.owned.empty() || r.data == nullptr))
+      r.data = reinterpret_cast<const uint8_t*>(r.owned.data());
     r.header_off = off;
     const bool z64_local = r.size >= U32MAX;
     r.zip64 = z64_local;
@@ -166,90 +319,52 @@ void ZipWriter::run(uintptr_t wait_event, bool do_fsync) {
     }
     const double t1 = now();
     stats_.wait_seconds = t1 - t0;
-    fd = ::open(tmp_.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
+    fd = ::open(tmp_.c_str(), O_WRONLY | O_CREAT | (truncate_ ? O_TRUNC : 0) | O_CLOEXEC, 0644);
     if (fd < 0) throw std::runtime_error("open(" + tmp_ + "): " + strerror(errno));
     int dfd_direct = -1;
     if (direct_) {
       dfd_direct = ::open(tmp_.c_str(), O_WRONLY | O_DIRECT | O_CLOEXEC);
       if (dfd_direct < 0) direct_used_ = false;  // filesystem without O_DIRECT: buffered only
     }
-    std::atomic<uint64_t> direct_bytes{0};
 
     // ---- data records: parallel CRC + pwrite in chunks --------------------------
-    struct Chunk {
-      size_t rec;
-      uint64_t off, len;
-      uint32_t crc;
-    };
-    std::vector<Chunk> chunks;
+    // (records whose bytes other ranks write — sharded save — carry a given CRC)
+    std::vector<FilePiece> pieces;
+    std::vector<std::pair<size_t, size_t>> rec_pieces(recs_.size(), {0, 0});
     for (size_t i = 0; i < recs_.size(); ++i) {
       const auto& r = recs_[i];
-      if (r.size == 0) chunks.push_back({i, 0, 0, 0});
-      for (uint64_t o = 0; o < r.size; o += chunk_) chunks.push_back({i, o, std::min(chunk_, r.size - o), 0});
-    }
-    std::atomic<size_t> next{0};
-    std::string err;
-    std::mutex err_mu;
-    auto worker = [&] {
-      for (;;) {
-        size_t k = next.fetch_add(1);
-        if (k >= chunks.size()) return;
-        Chunk& c = chunks[k];
-        const auto& r = recs_[c.rec];
-        try {
-          const uint8_t* p = r.data + c.off;
-          uLong crc = crc32(0L, Z_NULL, 0);
-          uint64_t done = 0;
-          while (done < c.len) {
-            const uInt n = (uInt)std::min<uint64_t>(c.len - done, 1u << 30);
-            crc = crc32(crc, p + done, n);
-            done += n;
-          }
-          c.crc = (uint32_t)crc;
-          if (c.len) {
-            const uint64_t foff = r.data_off + c.off;
-            const uint64_t body = (dfd_direct >= 0 && foff % DIRECT_ALIGN == 0 &&
-                                   reinterpret_cast<uintptr_t>(p) % DIRECT_ALIGN == 0)
-                                      ? c.len / DIRECT_ALIGN * DIRECT_ALIGN
-                                      : 0;
-            if (body) {
-              if (!pwrite_direct(dfd_direct, p, body, foff)) {
-                pwrite_all(fd, p, body, foff);  // O_DIRECT refused at write time
-              } else {
-                direct_bytes.fetch_add(body);
-              }
-            }
-            if (c.len > body) pwrite_all(fd, p + body, c.len - body, foff + body);
-          }
-        } catch (const std::exception& ex) {
-          std::lock_guard<std::mutex> g(err_mu);
-          err = ex.what();
-          next.store(chunks.size());
-        }
+      if (r.external) continue;
+      rec_pieces[i].first = pieces.size();
+      for (uint64_t o = 0; o < r.size; o += chunk_) {
+        FilePiece p;
+        p.file_off = r.data_off + o;
+        p.ptr = r.data + o;
+        p.len = std::min(chunk_, r.size - o);
+        pieces.push_back(p);
       }
-    };
-    std::vector<std::thread> pool;
-    const int nt = (int)std::min<size_t>(nthreads_, std::max<size_t>(1, chunks.size()));
-    for (int t = 0; t < nt; ++t) pool.emplace_back(worker);
-    for (auto& t : pool) t.join();
+      rec_pieces[i].second = pieces.size();
+    }
+    std::string err;
+    try {
+      stats_.direct_bytes = write_pieces_fd(fd, dfd_direct, pieces, nthreads_, chunk_);
+    } catch (const std::exception& ex) {
+      err = ex.what();
+    }
     if (dfd_direct >= 0) {
       if (do_fsync) ::fdatasync(dfd_direct);
       ::close(dfd_direct);
     }
-    stats_.direct_bytes = direct_bytes.load();
     if (!err.empty()) throw std::runtime_error(err);
-    for (auto& r : recs_) r.crc = 0;
-    {
-      std::vector<bool> first(recs_.size(), true);
-      for (const auto& c : chunks) {
-        auto& r = recs_[c.rec];
-        if (first[c.rec]) {
-          r.crc = c.crc;
-          first[c.rec] = false;
-        } else {
-          r.crc = (uint32_t)crc32_combine64(r.crc, c.crc, (z_off64_t)c.len);
-        }
+    for (size_t i = 0; i < recs_.size(); ++i) {
+      auto& r = recs_[i];
+      if (r.external) continue;
+      uint32_t crc = (uint32_t)crc32(0L, Z_NULL, 0);
+      bool first = true;
+      for (size_t k = rec_pieces[i].first; k < rec_pieces[i].second; ++k) {
+        crc = first ? pieces[k].crc : (uint32_t)crc32_combine64(crc, pieces[k].crc, (z_off64_t)pieces[k].len);
+        first = false;
       }
+      r.crc = crc;
     }
 
     // ---- local headers ----------------------------------------------------------

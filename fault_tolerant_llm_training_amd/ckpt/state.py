@@ -120,3 +120,32 @@ def restore_rng(r: Optional[Dict[str, Any]], device: torch.device) -> None:
         torch.set_rng_state(r["torch"])
     if device.type == "cuda" and "cuda" in r:
         torch.cuda.set_rng_state(r["cuda"], device)
+
+
+def shard_regions(model, optimizer, rank: int, world: int, align: int = 2048):
+    """This rank's pieces of (params, exp_avg, exp_avg_sq) for a sharded save.
+
+    Parameters (replicated): a contiguous 1/W slice, cut at ``align``-element (4 KiB)
+    boundaries so every rank's bytes start O_DIRECT-aligned in the file. AdamW moments:
+    under ZeRO-1 exactly the shards this rank owns (bucket by bucket); replicated
+    otherwise, 1/W slices like the parameters.
+    """
+    from .engine import Region
+
+    flat = model.flat
+    P = flat.numel
+
+    def cut(n):
+        bounds = [min(n, (n * i // world) // align * align) for i in range(world)] + [n]
+        return bounds[rank], bounds[rank + 1]
+
+    lo, hi = cut(P)
+    regions = [Region("params", flat.params[lo:hi], [(lo, 0, hi - lo)], P)]
+    if optimizer.zero1:
+        pieces = [(flo, slo, n) for flo, slo, n in optimizer.shard_pieces()]
+        regions.append(Region("exp_avg", optimizer.exp_avg, pieces, P))
+        regions.append(Region("exp_avg_sq", optimizer.exp_avg_sq, pieces, P))
+    else:
+        for name, buf in (("exp_avg", optimizer.exp_avg), ("exp_avg_sq", optimizer.exp_avg_sq)):
+            regions.append(Region(name, buf[lo:hi], [(lo, 0, hi - lo)], P))
+    return regions

@@ -28,6 +28,7 @@ class DistInfo:
     local_rank: int = 0
     device: torch.device = torch.device("cpu")
     ctrl_group: Optional[object] = None  # gloo group (None when world_size == 1)
+    ckpt_group: Optional[object] = None  # gloo group used only by checkpoint writer threads
 
     @property
     def is_main(self) -> bool:
@@ -76,6 +77,9 @@ def init_distributed(device_type: str = "cuda", timeout_s: int = 1800) -> DistIn
             else:
                 dist.init_process_group("gloo", timeout=timeout)
         info.ctrl_group = dist.new_group(backend="gloo", timeout=timeout) if device_type == "cuda" else dist.group.WORLD
+        # a second gloo group so background checkpoint-writer threads never interleave
+        # their collectives with the main thread's control-plane votes
+        info.ckpt_group = dist.new_group(backend="gloo", timeout=timeout)
     _INFO = info
     return info
 

@@ -36,7 +36,7 @@ import torch
 
 from .ckpt.engine import CheckpointEngine
 from .ckpt.format import checkpoint_file, load_checkpoint
-from .ckpt.state import build_checkpoint, capture_rng, restore_model, restore_rng
+from .ckpt.state import build_checkpoint, capture_rng, restore_model, restore_rng, shard_regions
 from .data.loader import IterableSource, MapSource, SyntheticSource, TrainLoader
 from .data.synthetic import SyntheticTokens
 from .ft.exit_handler import classify_exception, handle_exit
@@ -232,48 +232,53 @@ def train(args) -> int:
         logger.info(f"Data parallel over {info.world_size} ranks: {reducer.summary()}")
 
     ckpt_path = checkpoint_file(args.checkpoint_path, job_id)
-    ckpt = {"engine": None, "full": None}
+    ckpt = {"engine": None}
+    # FT_SHARDED_CKPT=1 forces the multi-writer protocol on a 1-rank process group (test hook)
+    sharded = info.world_size > 1 or (info.ckpt_group is not None and os.environ.get("FT_SHARDED_CKPT") == "1")
 
     def ckpt_engine():
         if ckpt["engine"] is None:
-            if optimizer.zero1:
-                # ZeRO-1: the moments are sharded; a full-layout copy is assembled in HBM at save time
-                ckpt["full"] = (torch.empty(model.flat.numel, dtype=optimizer.exp_avg.dtype, device=device),
-                                torch.empty(model.flat.numel, dtype=optimizer.exp_avg.dtype, device=device))
-                m, v = ckpt["full"]
+            if sharded:
+                # every rank writes its own pieces of the one file (ZeRO-1: its AdamW shards)
+                regions = shard_regions(model, optimizer, info.rank, info.world_size)
+                ckpt["engine"] = CheckpointEngine(regions, mode=args.checkpoint_mode,
+                                                  writer_threads=args.checkpoint_writer_threads,
+                                                  group=info.ckpt_group, rank=info.rank, world=info.world_size,
+                                                  sharded=True)
             else:
-                m, v = optimizer.exp_avg, optimizer.exp_avg_sq
-            ckpt["engine"] = CheckpointEngine({"params": model.flat.params, "exp_avg": m, "exp_avg_sq": v},
-                                              mode=args.checkpoint_mode,
-                                              writer_threads=args.checkpoint_writer_threads)
+                ckpt["engine"] = CheckpointEngine(
+                    {"params": model.flat.params, "exp_avg": optimizer.exp_avg, "exp_avg_sq": optimizer.exp_avg_sq},
+                    mode=args.checkpoint_mode, writer_threads=args.checkpoint_writer_threads)
         return ckpt["engine"]
 
     def save_checkpoint(blocking: bool, collective: bool = True):
         optimizer.gate.wait_all()  # the snapshot must follow this step's parameter updates
-        if optimizer.zero1 and not collective:
-            logger.error("ZeRO-1 optimizer state is sharded over the ranks; a rank-local error cannot "
-                         "write a complete checkpoint")
-            return False
-        engine = ckpt_engine()
-        if optimizer.zero1:
-            optimizer.gather_full_state(*ckpt["full"])
         if collective:
             states = fdist.ctrl_all_gather_object(loader.state_dict())
         else:  # rank-local save (error on this rank only): other ranks' positions unknown
             states = [None] * info.world_size
             states[info.rank] = loader.state_dict()
-        writer = info.is_main if collective else True
-        st = None
-        if writer:
-            step_now = training_step
-            rng = capture_rng(device)
+        step_now = training_step
+        rng = capture_rng(device)
 
-            def build(host):
-                return build_checkpoint(model, optimizer, lr_scheduler, step_now, host,
-                                        data_loader=states if info.distributed else states[0], rng=rng,
-                                        extra_meta={"world_size": info.world_size, "job_id": str(job_id)})
+        def build(host):
+            return build_checkpoint(model, optimizer, lr_scheduler, step_now, host,
+                                    data_loader=states if info.distributed else states[0], rng=rng,
+                                    extra_meta={"world_size": info.world_size, "job_id": str(job_id)})
 
-            st = engine.save(ckpt_path, build, step=step_now, blocking=blocking)
+        if sharded and not collective:
+            if optimizer.zero1:
+                logger.error("ZeRO-1 optimizer state is sharded over the ranks; a rank-local error cannot "
+                             "write a complete checkpoint")
+                return False
+            # replicated state: this rank writes the whole file alone
+            solo = CheckpointEngine({"params": model.flat.params, "exp_avg": optimizer.exp_avg,
+                                     "exp_avg_sq": optimizer.exp_avg_sq}, mode="host",
+                                    writer_threads=args.checkpoint_writer_threads)
+            return solo.save(ckpt_path, build, step=step_now, blocking=True)
+        engine = ckpt_engine()
+        writes = sharded or info.is_main
+        st = engine.save(ckpt_path, build, step=step_now, blocking=blocking) if writes else None
         if collective and blocking:
             fdist.barrier()
         return st

@@ -167,3 +167,20 @@ def test_dp_signal_to_one_rank_stops_all_and_resume_is_exact(tmp_path, mode):
         assert torch.equal(a["model"][k], b["model"][k]), k
     for i in a["optimizer"]["state"]:
         assert torch.equal(a["optimizer"]["state"][i]["exp_avg_sq"], b["optimizer"]["state"][i]["exp_avg_sq"])
+
+
+def test_resume_dp2_checkpoint_on_one_rank_and_back(tmp_path):
+    """The checkpoint is full-layout (ZeRO-1 shards are gathered), so the world size may change."""
+    d = str(tmp_path)
+    write_fake_sbatch(d)
+    ck = ["--checkpoint-path", os.path.join(d, "ck")]
+    base = TINY + ["--synthetic-data", "--vocab-size", "256", "--training-steps", "40", "--dp-bucket-mb", "0.1"] + ck
+    rc, out = _run(d, "400", base + ["--raise-error", "--error-step", "6"])
+    assert rc == 0 and "Checkpoint saved at step 6" in out, out
+    from helpers import run_train
+
+    rc, out = run_train(d, "401", base + ["--checkpoint-id", "400", "--raise-error", "--error-step", "9"])
+    assert rc == 0 and "Resuming training from training_step 6" in out and "Checkpoint saved at step 9" in out, out
+    assert "written by 2 ranks, resuming on 1" in out
+    rc, out = _run(d, "402", base + ["--checkpoint-id", "401", "--raise-error", "--error-step", "12"])
+    assert rc == 0 and "Resuming training from training_step 9" in out and "Checkpoint saved at step 12" in out, out
