@@ -99,7 +99,9 @@ def restore_model(model, sd: Dict[str, torch.Tensor]) -> str:
         raise KeyError(f"checkpoint/model mismatch: missing={missing[:5]} unexpected={unexpected[:5]}")
     src = _flat_source(sd, flat.slots, flat.numel, flat.dtype)
     if src is not None:
-        flat.params.copy_(src, non_blocking=True)
+        from .restore import h2d
+
+        h2d(flat.params, src)
         return "flat"
     for name in expected:
         _view(flat.params, flat.slots[name]).copy_(sd[name], non_blocking=True)

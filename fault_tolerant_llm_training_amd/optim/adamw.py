@@ -274,11 +274,13 @@ class FlatAdamW(torch.optim.Optimizer):
                 for i, t in tensors.items():
                     s = slots_by_idx[i]
                     src[s.offset : s.offset + s.numel].view(s.shape).copy_(t)
+            from ..ckpt.restore import h2d
+
             if self.zero1:
                 for flo, slo, n in self.shard_pieces():
-                    buf[slo : slo + n].copy_(src[flo : flo + n], non_blocking=True)
+                    h2d(buf[slo : slo + n], src[flo : flo + n])
             else:
-                buf.copy_(src, non_blocking=True)
+                h2d(buf, src)
         steps = {int(float(st[i]["step"])) for i in slots_by_idx if i in st}
         if steps:
             self.step_count = max(steps)

@@ -221,6 +221,9 @@ def train(args) -> int:
         training_step = 0
         logger.info("Starting training!")
     del checkpoint
+    from .ckpt.restore import release as _release_restore_ring
+
+    _release_restore_ring()
 
     if info.distributed:
         if training_step == 0:

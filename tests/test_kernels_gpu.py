@@ -238,3 +238,14 @@ def test_add_norm_fused(ln):
     assert rel(h, hr) < 1e-2 and rel(y, yr) < 1e-2
     assert rel(x.grad, xr.grad) < 2e-2 and torch.equal(x.grad, d.grad)
     assert rel(w.grad, wr.grad) < 2e-2
+
+
+def test_pinned_ring_h2d():
+    from fault_tolerant_llm_training_amd.ckpt.restore import h2d, release
+
+    src = torch.randn(300 * (1 << 20) // 2).bfloat16()  # 300 MiB: > 1 chunk, ragged tail
+    dst = torch.empty(src.numel(), dtype=torch.bfloat16, device="cuda")
+    h2d(dst, src, min_bytes=0)
+    torch.cuda.synchronize()
+    assert torch.equal(dst.cpu(), src)
+    release()
