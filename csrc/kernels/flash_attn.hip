@@ -32,6 +32,7 @@
 // XCD L2 under round-robin dispatch; a speed choice only).
 #include "torch_utils.h"
 
+#include <type_traits>
 #include <utility>
 
 namespace {
@@ -138,6 +139,10 @@ __device__ __forceinline__ f32x16_t mfma32(bf16x8_t a, bf16x8_t b, f32x16_t c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
 
+// Raw v_exp_f32 (2^x): exp2f adds denormal range-reduction (cmp + cndmask + ldexp per
+// call) that softmax does not need — its arguments are <= 0 and tiny results flush to 0.
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
 __device__ __forceinline__ void map_head(int hh, int Hq, int Hkv, int& h, int& kvh) {
   // hh in [0, Hq) -> (h, kvh) so that the Hq/Hkv siblings of one KV head are
   // Hkv block-ids apart (same XCD when Hkv == 8).
@@ -194,19 +199,27 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(const bf16_t* __restr
   const int kend = min((qt + 1) * BM, S);
   const int ntiles = (kend + BN - 1) / BN;
   u32x4 kr[CPT], vr[CPT];
+  // loop-invariant per-thread staging coordinates (row within the tile, 16-B chunk)
+  int srow[CPT], soff[CPT];
+  static_for<CPT>([&](auto I) {
+    const int id = tid + I * 256;
+    srow[I] = id / DCH;
+    soff[I] = lds_off<D>(id / DCH, id % DCH);
+  });
+  static_assert(256 % DCH == 0, "staging chunk must be the same for every I");
+  const bf16_t* Kc = Kg + (tid % DCH) * 8;  // 256 is a multiple of DCH: same chunk for all I
+  const bf16_t* Vc = Vg + (tid % DCH) * 8;
 #define FWD_GLOAD(KT)                                                        \
   static_for<CPT>([&](auto I) {                                              \
-    const int id = tid + I * 256, row = id / DCH, c = id % DCH;              \
-    const long key = min((KT) * BN + row, S - 1);                            \
-    kr[I] = *reinterpret_cast<const u32x4*>(Kg + key * ldqk + c * 8);        \
-    vr[I] = *reinterpret_cast<const u32x4*>(Vg + key * ldv + c * 8);         \
+    const long key = min((KT) * BN + srow[I], S - 1);                        \
+    kr[I] = *reinterpret_cast<const u32x4*>(Kc + key * ldqk);                \
+    vr[I] = *reinterpret_cast<const u32x4*>(Vc + key * ldv);                 \
   });
 #define FWD_SWRITE(BUF)                                                      \
   static_for<CPT>([&](auto I) {                                              \
-    const int id = tid + I * 256, row = id / DCH, c = id % DCH;              \
     char* kb_ = smem + (BUF) * 2 * TILE;                                     \
-    *reinterpret_cast<u32x4*>(kb_ + lds_off<D>(row, c)) = kr[I];             \
-    *reinterpret_cast<u32x4*>(kb_ + TILE + lds_off<D>(row, c)) = vr[I];      \
+    *reinterpret_cast<u32x4*>(kb_ + soff[I]) = kr[I];                        \
+    *reinterpret_cast<u32x4*>(kb_ + TILE + soff[I]) = vr[I];                 \
   });
 
   FWD_GLOAD(0)
@@ -230,43 +243,45 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(const bf16_t* __restr
     const int k0 = kt * BN;
     const bool v0 = k0 <= q0 + 31;       // wave-uniform: sub-tile 0 has an unmasked key
     const bool v1 = k0 + 32 <= q0 + 31;  // sub-tile 1
-    if (v0) {
+    // Two code paths: tiles strictly below the diagonal need no masking at all
+    // (most of them), diagonal tiles mask per element. Wave-uniform branch.
+    auto tile = [&](auto MASKED) {
+      constexpr bool MASK = decltype(MASKED)::value;
       f32x16_t s[2];
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) s[j][r] = 0.f;
-        if (j == 0 || v1) {
+        if (!MASK || j == 0 || v1) {
 #pragma unroll
           for (int ks = 0; ks < KS; ++ks)
             s[j] = mfma32(ld_row<D>(kb, j * 32 + l32, 2 * ks + hi), qf[ks], s[j]);
         }
       }
+      // max over raw scores (the softmax scale is > 0), scale folded into one FMA below
       float mx = -INFINITY;
-      const bool diag = k0 + BN - 1 > q0;  // some key may exceed some query of this wave
 #pragma unroll
       for (int j = 0; j < 2; ++j)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          float x = s[j][r] * sl2;
-          if (j == 1 && !v1) x = -INFINITY;
-          if (diag) {
+          float x = s[j][r];
+          if constexpr (MASK) {
             const int key = k0 + j * 32 + (r & 3) + 8 * (r >> 2) + 4 * hi;
-            if (key > qrow) x = -INFINITY;
+            if ((j == 1 && !v1) || key > qrow) x = -INFINITY;
+            s[j][r] = x;
           }
-          s[j][r] = x;
           mx = fmaxf(mx, x);
         }
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float mn = fmaxf(m, mx);
-      const float alpha = exp2f(m - mn);
+      const float mn = fmaxf(m, mx * sl2);
+      const float alpha = fast_exp2(m - mn);
       m = mn;
       float ls = 0.f;
 #pragma unroll
       for (int j = 0; j < 2; ++j)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const float p = exp2f(s[j][r] - mn);
+          const float p = fast_exp2(fmaf(s[j][r], sl2, -mn));
           ls += p;
           s[j][r] = p;
         }
@@ -282,13 +297,19 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(const bf16_t* __restr
         o[db] = mfma32(tr_frag<D>(vb, 0, db * 32, lane), pb00, o[db]);
         o[db] = mfma32(tr_frag<D>(vb, 16, db * 32, lane), pb01, o[db]);
       }
-      if (v1) {
+      if (!MASK || v1) {
 #pragma unroll
         for (int db = 0; db < NDB; ++db) {
           o[db] = mfma32(tr_frag<D>(vb, 32, db * 32, lane), pb10, o[db]);
           o[db] = mfma32(tr_frag<D>(vb, 48, db * 32, lane), pb11, o[db]);
         }
       }
+    };
+    if (v0) {
+      if (k0 + BN - 1 > q0)  // some key may exceed some query of this wave
+        tile(std::true_type{});
+      else
+        tile(std::false_type{});
     }
     if (kt + 1 < ntiles) {
       FWD_SWRITE(cur ^ 1)
@@ -474,7 +495,7 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_kernel(
         for (int t = 0; t < 4; ++t) {
           const int r = 4 * g + t;
           const int q = qb + 8 * g + 4 * hi + t;
-          float p = exp2f(s[r] * sl2 - lv[t]);
+          float p = fast_exp2(fmaf(s[r], sl2, -lv[t]));
           if (key > q || q >= S) p = 0.f;
           dp[r] = p * (dp[r] - dv4[t]);
           s[r] = p;
@@ -599,19 +620,25 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dq_kernel(
   const int kend = min((qt + 1) * BM, S);
   const int ntiles = (kend + BN - 1) / BN;
   u32x4 kr[CPT], vr[CPT];
+  int srow[CPT], soff[CPT];
+  static_for<CPT>([&](auto I) {
+    const int id = tid + I * 256;
+    srow[I] = id / DCH;
+    soff[I] = lds_off<D>(id / DCH, id % DCH);
+  });
+  const bf16_t* Kc = Kg + (tid % DCH) * 8;
+  const bf16_t* Vc = Vg + (tid % DCH) * 8;
 #define DQ_GLOAD(KT)                                                         \
   static_for<CPT>([&](auto I) {                                              \
-    const int id = tid + I * 256, row = id / DCH, c = id % DCH;              \
-    const long key = min((KT) * BN + row, S - 1);                            \
-    kr[I] = *reinterpret_cast<const u32x4*>(Kg + key * ldqk + c * 8);        \
-    vr[I] = *reinterpret_cast<const u32x4*>(Vg + key * ldv + c * 8);         \
+    const long key = min((KT) * BN + srow[I], S - 1);                        \
+    kr[I] = *reinterpret_cast<const u32x4*>(Kc + key * ldqk);                \
+    vr[I] = *reinterpret_cast<const u32x4*>(Vc + key * ldv);                 \
   });
 #define DQ_SWRITE(BUF)                                                       \
   static_for<CPT>([&](auto I) {                                              \
-    const int id = tid + I * 256, row = id / DCH, c = id % DCH;              \
     char* kb_ = smem + (BUF) * 2 * TILE;                                     \
-    *reinterpret_cast<u32x4*>(kb_ + lds_off<D>(row, c)) = kr[I];             \
-    *reinterpret_cast<u32x4*>(kb_ + TILE + lds_off<D>(row, c)) = vr[I];      \
+    *reinterpret_cast<u32x4*>(kb_ + soff[I]) = kr[I];                        \
+    *reinterpret_cast<u32x4*>(kb_ + TILE + soff[I]) = vr[I];                 \
   });
 
   DQ_GLOAD(0)
@@ -634,13 +661,14 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dq_kernel(
     const int k0 = kt * BN;
     const bool v0 = k0 <= q0 + 31;
     const bool v1 = k0 + 32 <= q0 + 31;
-    if (v0) {
+    auto tile = [&](auto MASKED) {
+      constexpr bool MASK = decltype(MASKED)::value;
       f32x16_t sc[2], dp[2];
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) sc[j][r] = dp[j][r] = 0.f;
-        if (j == 0 || v1) {
+        if (!MASK || j == 0 || v1) {
 #pragma unroll
           for (int ks = 0; ks < KS; ++ks) {
             sc[j] = mfma32(ld_row<D>(kb, j * 32 + l32, 2 * ks + hi), qf[ks], sc[j]);
@@ -648,18 +676,15 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dq_kernel(
           }
         }
       }
-      const bool diag = k0 + BN - 1 > q0;
 #pragma unroll
       for (int j = 0; j < 2; ++j)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          float p = exp2f(sc[j][r] * sl2 - lq);
-          if (j == 1 && !v1) p = 0.f;
-          if (diag) {
+          float p = fast_exp2(fmaf(sc[j][r], sl2, -lq));
+          if constexpr (MASK) {
             const int key = k0 + j * 32 + (r & 3) + 8 * (r >> 2) + 4 * hi;
-            if (key > qrow) p = 0.f;
+            if ((j == 1 && !v1) || key > qrow || qrow >= S) p = 0.f;
           }
-          if (qrow >= S) p = 0.f;
           sc[j][r] = p * (dp[j][r] - dlq);
         }
       const bf16x8_t d00 = cvt8<0>(sc[0]), d01 = cvt8<8>(sc[0]);
@@ -669,13 +694,20 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dq_kernel(
         dq[db] = mfma32(tr_frag<D>(kb, 0, db * 32, lane), d00, dq[db]);
         dq[db] = mfma32(tr_frag<D>(kb, 16, db * 32, lane), d01, dq[db]);
       }
-      if (v1) {
+      if (!MASK || v1) {
 #pragma unroll
         for (int db = 0; db < NDB; ++db) {
           dq[db] = mfma32(tr_frag<D>(kb, 32, db * 32, lane), d10, dq[db]);
           dq[db] = mfma32(tr_frag<D>(kb, 48, db * 32, lane), d11, dq[db]);
         }
       }
+    };
+    if (v0) {
+      // rows >= S (ragged last tile) take the masked path too
+      if (k0 + BN - 1 > q0 || q0 + 31 >= S)
+        tile(std::true_type{});
+      else
+        tile(std::false_type{});
     }
     if (kt + 1 < ntiles) {
       DQ_SWRITE(cur ^ 1)
