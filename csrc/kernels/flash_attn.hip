@@ -475,7 +475,8 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_kernel(
     const float* dl = ls + 32;
     const int qb = qs * BQ;
     const bool active = qb + BQ - 1 >= kw;  // wave-uniform
-    if (active) {
+    auto slice = [&](auto MASKED) {
+      constexpr bool MASK = decltype(MASKED)::value;
       f32x16_t s, dp;
 #pragma unroll
       for (int r = 0; r < 16; ++r) s[r] = dp[r] = 0.f;
@@ -494,9 +495,11 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_kernel(
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
           const int r = 4 * g + t;
-          const int q = qb + 8 * g + 4 * hi + t;
           float p = fast_exp2(fmaf(s[r], sl2, -lv[t]));
-          if (key > q || q >= S) p = 0.f;
+          if constexpr (MASK) {
+            const int q = qb + 8 * g + 4 * hi + t;
+            if (key > q || q >= S) p = 0.f;
+          }
           dp[r] = p * (dp[r] - dv4[t]);
           s[r] = p;
         }
@@ -510,16 +513,25 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_kernel(
           dv[db] = mfma32(pa[ss], tr_frag<D>(di, 16 * ss, db * 32, lane), dv[db]);
           dk[db] = mfma32(da[ss], tr_frag<D>(qi, 16 * ss, db * 32, lane), dk[db]);
         }
-      // dS -> LDS image [key][q] (4 x 8-B writes per lane)
-      char* row = dsimg + (wave * 32 + l32) * 64;
+      if constexpr (DQ != 1) {
+        // dS -> LDS image [key][q] (4 x 8-B writes per lane) for the in-kernel dQ stage
+        char* row = dsimg + (wave * 32 + l32) * 64;
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        uint2 v;
-        v.x = pack2(dp[4 * g + 0], dp[4 * g + 1]);
-        v.y = pack2(dp[4 * g + 2], dp[4 * g + 3]);
-        *reinterpret_cast<uint2*>(row + (8 * g + 4 * hi) * 2) = v;
+        for (int g = 0; g < 4; ++g) {
+          uint2 v;
+          v.x = pack2(dp[4 * g + 0], dp[4 * g + 1]);
+          v.y = pack2(dp[4 * g + 2], dp[4 * g + 3]);
+          *reinterpret_cast<uint2*>(row + (8 * g + 4 * hi) * 2) = v;
+        }
       }
-    } else {
+    };
+    if (active) {
+      // the slice straddles this wave's keys (or the ragged end): mask per element
+      if (kw + 31 > qb || qb + BQ > S)
+        slice(std::true_type{});
+      else
+        slice(std::false_type{});
+    } else if constexpr (DQ != 1) {
       char* row = dsimg + (wave * 32 + l32) * 64;
 #pragma unroll
       for (int g = 0; g < 4; ++g) *reinterpret_cast<uint2*>(row + (8 * g + 4 * hi) * 2) = make_uint2(0, 0);
