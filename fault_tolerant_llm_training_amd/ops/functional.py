@@ -90,6 +90,9 @@ class EmbeddingFn(torch.autograd.Function):
         (tokens,) = ctx.saved_tensors
         sink = ctx.sink
         dy = dy.contiguous()
+        if sink is not None and sink.gather is not None:
+            # DP sparse exchange: every rank's (token, dY) rows, scatter-added locally
+            tokens, dy = sink.gather(tokens, dy)
         if dy.is_cuda:
             if sink is None:
                 dw = torch.zeros(ctx.wshape, dtype=dy.dtype, device=dy.device)

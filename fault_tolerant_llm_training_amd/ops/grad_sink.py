@@ -15,7 +15,7 @@ import torch
 
 
 class GradSink:
-    __slots__ = ("buf", "start", "end", "accumulate", "hook", "name")
+    __slots__ = ("buf", "start", "end", "accumulate", "hook", "name", "gather")
 
     def __init__(self, buf: torch.Tensor, start: int = 0, end: int = 0, name: str = ""):
         self.buf = buf
@@ -24,6 +24,8 @@ class GradSink:
         self.accumulate = False  # True for micro-batches after the first (grad accumulation)
         self.hook: Optional[Callable[["GradSink"], None]] = None
         self.name = name
+        # data parallel: (tokens, dy) -> every rank's (tokens, dy) (sparse embedding exchange)
+        self.gather: Optional[Callable] = None
 
     def ready(self) -> None:
         if self.hook is not None:

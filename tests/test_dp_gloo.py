@@ -55,12 +55,13 @@ def _worker(rank, world, port, out_dir, bucket_mb, mode):
         loss.backward()
         ddp.finish()
     if mode == "allreduce":
+        assert any(b.sparse for b in ddp.buckets)  # the embedding is exchanged sparsely
         torch.save(m.flat.grads.clone(), os.path.join(out_dir, f"g{rank}.pt"))
     else:  # scatter this rank's reduced shards back into a full-layout tensor
         full = torch.full_like(m.flat.grads, float("nan"))
         for b in ddp.buckets:
             lo = b.lo + rank * b.shard_len
-            full[lo : lo + b.shard_len] = ddp.grad_shard[b.shard_lo : b.shard_lo + b.shard_len]
+            full[lo : lo + b.shard_len] = ddp.grad_for_update(b)
         torch.save(full, os.path.join(out_dir, f"g{rank}.pt"))
     dist.destroy_process_group()
 
