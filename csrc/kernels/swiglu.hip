@@ -54,6 +54,97 @@ __global__ __launch_bounds__(256) void swiglu_bwd_kernel(const bf16_t* __restric
   }
 }
 
+// Tiled variants that also write the transposed output, which the weight-gradient
+// GEMMs consume in their fast K-contiguous ("TN") layout: one 64 x 64 tile per block,
+// the transpose goes through LDS, both stores are 16-B vectors. Saves the separate
+// transpose kernel's full read of the activation (ops/functional.py: weight_grad).
+constexpr int TT = 64;
+
+__global__ __launch_bounds__(256) void swiglu_fwd_t_kernel(const bf16_t* __restrict__ gu,
+                                                           bf16_t* __restrict__ a,
+                                                           bf16_t* __restrict__ aT, int T, int F) {
+  __shared__ bf16_t tile[TT][TT + 2];
+  const int tilesF = F / TT;
+  const int r0 = (blockIdx.x / tilesF) * TT, c0 = (blockIdx.x % tilesF) * TT;
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int id = t + k * 256, row = id >> 3, seg = id & 7;
+    const long base = (long)(r0 + row) * 2 * F + c0 + seg * 8;
+    float g[8], u[8], o[8];
+    unpack8(*reinterpret_cast<const uint4*>(gu + base), g);
+    unpack8(*reinterpret_cast<const uint4*>(gu + base + F), u);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = g[j] * sigmoidf_(g[j]) * u[j];
+    const uint4 v = pack8(o);
+    *reinterpret_cast<uint4*>(a + (long)(r0 + row) * F + c0 + seg * 8) = v;
+    const bf16_t* e = reinterpret_cast<const bf16_t*>(&v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) tile[row][seg * 8 + j] = e[j];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int id = t + k * 256, c = id >> 3, seg = id & 7;
+    uint4 v;
+    bf16_t* e = reinterpret_cast<bf16_t*>(&v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) e[j] = tile[seg * 8 + j][c];
+    *reinterpret_cast<uint4*>(aT + (long)(c0 + c) * T + r0 + seg * 8) = v;
+  }
+}
+
+__global__ __launch_bounds__(256) void swiglu_bwd_t_kernel(const bf16_t* __restrict__ da,
+                                                           const bf16_t* __restrict__ gu,
+                                                           bf16_t* __restrict__ dgu,
+                                                           bf16_t* __restrict__ dguT, int T, int F) {
+  __shared__ bf16_t tg[TT][TT + 2], tu[TT][TT + 2];
+  const int tilesF = F / TT;
+  const int r0 = (blockIdx.x / tilesF) * TT, c0 = (blockIdx.x % tilesF) * TT;
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int id = t + k * 256, row = id >> 3, seg = id & 7;
+    const long base = (long)(r0 + row) * 2 * F + c0 + seg * 8;
+    float g[8], u[8], d[8], dg[8], du[8];
+    unpack8(*reinterpret_cast<const uint4*>(gu + base), g);
+    unpack8(*reinterpret_cast<const uint4*>(gu + base + F), u);
+    unpack8(*reinterpret_cast<const uint4*>(da + (long)(r0 + row) * F + c0 + seg * 8), d);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float s = sigmoidf_(g[j]);
+      const float silu = g[j] * s;
+      du[j] = d[j] * silu;
+      dg[j] = d[j] * u[j] * (s + silu * (1.f - s));
+    }
+    const uint4 vg = pack8(dg), vu = pack8(du);
+    *reinterpret_cast<uint4*>(dgu + base) = vg;
+    *reinterpret_cast<uint4*>(dgu + base + F) = vu;
+    const bf16_t* eg = reinterpret_cast<const bf16_t*>(&vg);
+    const bf16_t* eu = reinterpret_cast<const bf16_t*>(&vu);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      tg[row][seg * 8 + j] = eg[j];
+      tu[row][seg * 8 + j] = eu[j];
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int id = t + k * 256, c = id >> 3, seg = id & 7;
+    uint4 vg, vu;
+    bf16_t* eg = reinterpret_cast<bf16_t*>(&vg);
+    bf16_t* eu = reinterpret_cast<bf16_t*>(&vu);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      eg[j] = tg[seg * 8 + j][c];
+      eu[j] = tu[seg * 8 + j][c];
+    }
+    *reinterpret_cast<uint4*>(dguT + (long)(c0 + c) * T + r0 + seg * 8) = vg;
+    *reinterpret_cast<uint4*>(dguT + (long)(F + c0 + c) * T + r0 + seg * 8) = vu;
+  }
+}
+
 int grid_for(long work) {
   long g = (work + 255) / 256;
   return (int)std::max(1L, std::min(g, 256L * 16));
@@ -100,7 +191,47 @@ at::Tensor swiglu_bwd(const at::Tensor& da, const at::Tensor& gu) {
   return dgu;
 }
 
+// (a [T, F], a^T [F, T]); T and F multiples of 64.
+std::tuple<at::Tensor, at::Tensor> swiglu_fwd_t(const at::Tensor& gu) {
+  FT_CHECK_CUDA(gu);
+  FT_CHECK_BF16(gu);
+  FT_CHECK_CONTIG(gu);
+  const int F = gu.size(-1) / 2;
+  const int T = gu.numel() / (2 * F);
+  TORCH_CHECK(F % TT == 0 && T % TT == 0, "swiglu_fwd_t: T and F must be multiples of 64");
+  const at::DeviceGuard guard(gu.device());
+  auto a = at::empty({T, F}, gu.options());
+  auto aT = at::empty({F, T}, gu.options());
+  if (T > 0)
+    hipLaunchKernelGGL(swiglu_fwd_t_kernel, dim3((T / TT) * (F / TT)), dim3(256), 0, ft_stream(),
+                       cptr<bf16_t>(gu), mptr<bf16_t>(a), mptr<bf16_t>(aT), T, F);
+  FT_LAUNCH_CHECK();
+  return {a, aT};
+}
+
+// (dgu [T, 2F], dgu^T [2F, T]); T and F multiples of 64.
+std::tuple<at::Tensor, at::Tensor> swiglu_bwd_t(const at::Tensor& da, const at::Tensor& gu) {
+  FT_CHECK_CUDA(gu);
+  FT_CHECK_BF16(gu);
+  FT_CHECK_CONTIG(gu);
+  FT_CHECK_CONTIG(da);
+  const int F = gu.size(-1) / 2;
+  const int T = gu.numel() / (2 * F);
+  TORCH_CHECK(da.numel() == (long)T * F, "swiglu_bwd_t: shape mismatch");
+  TORCH_CHECK(F % TT == 0 && T % TT == 0, "swiglu_bwd_t: T and F must be multiples of 64");
+  const at::DeviceGuard guard(gu.device());
+  auto dgu = at::empty({T, 2 * F}, gu.options());
+  auto dguT = at::empty({2 * F, T}, gu.options());
+  if (T > 0)
+    hipLaunchKernelGGL(swiglu_bwd_t_kernel, dim3((T / TT) * (F / TT)), dim3(256), 0, ft_stream(),
+                       cptr<bf16_t>(da), cptr<bf16_t>(gu), mptr<bf16_t>(dgu), mptr<bf16_t>(dguT), T, F);
+  FT_LAUNCH_CHECK();
+  return {dgu, dguT};
+}
+
 TORCH_LIBRARY_FRAGMENT(ftamd, m) {
+  m.def("swiglu_fwd_t(Tensor gu) -> (Tensor, Tensor)", &swiglu_fwd_t);
+  m.def("swiglu_bwd_t(Tensor da, Tensor gu) -> (Tensor, Tensor)", &swiglu_bwd_t);
   m.def("swiglu_fwd(Tensor gu) -> Tensor", &swiglu_fwd);
   m.def("swiglu_bwd(Tensor da, Tensor gu) -> Tensor", &swiglu_bwd);
 }

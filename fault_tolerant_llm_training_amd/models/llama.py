@@ -145,9 +145,7 @@ class TransformerBlock(nn.Module):
         o = Fx.rope_attention(qkv.view(-1, qkv.shape[-1]), cos, sin, seq_len, at.n_heads, at.n_kv_heads, at.head_dim)
         da = Fx.linear(o.view(*h.shape[:-1], -1), at.wo.weight, sk(at.wo.weight))
         h, hn = Fx.add_norm(h, da, self.ffn_norm.weight, sk(self.ffn_norm.weight), self.eps, self.layernorm)
-        gu = Fx.linear(hn, ff.w13, ff.w13_sink)
-        a = Fx.swiglu(gu)
-        return h, Fx.linear(a, ff.w2.weight, sk(ff.w2.weight))
+        return h, Fx.feed_forward(hn, ff.w13, ff.w2.weight, ff.w13_sink, sk(ff.w2.weight))
 
 
 class Transformer(nn.Module):

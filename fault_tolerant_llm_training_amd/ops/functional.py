@@ -47,12 +47,18 @@ def _use_tn(dy2: torch.Tensor, x2: torch.Tensor) -> bool:
     return _DW_MODE == "all" or 2.0 * T * N * K >= _DW_MIN_FLOP
 
 
-def weight_grad(dy2: torch.Tensor, x2: torch.Tensor, sink: Optional[GradSink]):
-    """dW[N, K] = dy2[T, N]^T @ x2[T, K], into the sink (flat grad buffer) or returned."""
+def weight_grad(dy2: torch.Tensor, x2: torch.Tensor, sink: Optional[GradSink],
+                dyT: Optional[torch.Tensor] = None, xT: Optional[torch.Tensor] = None):
+    """dW[N, K] = dy2[T, N]^T @ x2[T, K], into the sink (flat grad buffer) or returned.
+
+    ``dyT`` / ``xT``: already-transposed operands written by a producer kernel (the fused
+    SwiGLU kernels), used instead of running the transpose kernel. ``x2`` may then be None."""
+    if xT is not None and x2 is None:
+        x2 = xT.t()
     if _use_tn(dy2, x2):
         K_ = kernels()
-        a = K_.transpose2d(dy2.contiguous())   # [N, T]
-        b = K_.transpose2d(x2.contiguous())    # [K, T]
+        a = dyT if dyT is not None else K_.transpose2d(dy2.contiguous())   # [N, T]
+        b = xT if xT is not None else K_.transpose2d(x2.contiguous())      # [K, T]
         if sink is not None:
             sink.mm(a, b.t())
             return None
@@ -336,6 +342,63 @@ class SwiGLUFn(torch.autograd.Function):
 
 def swiglu(gu):
     return SwiGLUFn.apply(gu)
+
+
+_FUSED_FFN = os.environ.get("FT_FUSED_FFN", "1") != "0"
+
+
+class FeedForwardFn(torch.autograd.Function):
+    """x → [w1; w3] GEMM → SwiGLU → w2 GEMM as one autograd node (GPU, 64-multiple shapes).
+
+    The tiled SwiGLU kernels also emit the transposed activation ``a^T`` (forward) and
+    ``dgu^T`` (backward), the K-contiguous operands of the w2 and w13 weight-gradient GEMMs,
+    so neither needs a separate transpose pass; only ``a^T`` is kept for backward (``a``
+    itself is freed right after the w2 GEMM). Reference math: model.py:253-254."""
+
+    @staticmethod
+    def forward(ctx, x, w13, w2, sink13, sink2):
+        K_ = kernels()
+        D = x.shape[-1]
+        x2 = x.reshape(-1, D)
+        gu = torch.mm(x2, w13.t())
+        tn = _use_tn(gu, x2)
+        if tn:
+            a, aT = K_.swiglu_fwd_t(gu)
+        else:
+            a, aT = K_.swiglu_fwd(gu), None
+        y = torch.mm(a, w2.t())
+        ctx.sinks = (sink13, sink2)
+        ctx.tn = tn
+        ctx.xshape = x.shape
+        ctx.save_for_backward(x2, gu, aT if tn else a, w13, w2)
+        return y.view(*x.shape[:-1], w2.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, gu, a_or_T, w13, w2 = ctx.saved_tensors
+        sink13, sink2 = ctx.sinks
+        K_ = kernels()
+        dy2 = dy.reshape(-1, w2.shape[0]).contiguous()
+        if ctx.tn:
+            dw2 = weight_grad(dy2, None, sink2, xT=a_or_T)
+        else:
+            dw2 = weight_grad(dy2, a_or_T, sink2)
+        da = torch.mm(dy2, w2)
+        if ctx.tn:
+            dgu, dguT = K_.swiglu_bwd_t(da, gu)
+        else:
+            dgu, dguT = K_.swiglu_bwd(da, gu), None
+        del da
+        dw13 = weight_grad(dgu, x2, sink13, dyT=dguT)
+        dx = torch.mm(dgu, w13).view(ctx.xshape)
+        return dx, dw13, dw2, None, None
+
+
+def feed_forward(x, w13, w2, sink13=None, sink2=None):
+    """SwiGLU FFN on the fused [w1; w3] weight; fused node on the GPU, composed ops on CPU."""
+    if _FUSED_FFN and x.is_cuda and w13.shape[0] % 128 == 0 and x.numel() // x.shape[-1] % 64 == 0:
+        return FeedForwardFn.apply(x, w13, w2, sink13, sink2)
+    return linear(swiglu(linear(x, w13, sink13)), w2, sink2)
 
 
 # --------------------------------------------------------------------------------------

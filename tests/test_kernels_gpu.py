@@ -249,3 +249,43 @@ def test_pinned_ring_h2d():
     torch.cuda.synchronize()
     assert torch.equal(dst.cpu(), src)
     release()
+
+
+@pytest.mark.parametrize("T,F_", [(64, 64), (192, 320), (512, 1408)])
+def test_swiglu_transposed_outputs(K, T, F_):
+    """Tiled SwiGLU kernels: the row-major outputs equal the elementwise kernels' bitwise,
+    and the extra transposed outputs are exact transposes."""
+    gu = torch.randn(T, 2 * F_, device="cuda").bfloat16()
+    a, aT = K.swiglu_fwd_t(gu)
+    assert torch.equal(a, K.swiglu_fwd(gu)) and torch.equal(aT, a.t().contiguous())
+    da = torch.randn(T, F_, device="cuda").bfloat16()
+    dgu, dguT = K.swiglu_bwd_t(da, gu)
+    assert torch.equal(dgu, K.swiglu_bwd(da, gu)) and torch.equal(dguT, dgu.t().contiguous())
+
+
+@pytest.mark.parametrize("mode", ["all", "none"])
+def test_feed_forward_fused(mode, monkeypatch):
+    """FeedForwardFn (GEMM → tiled SwiGLU with transposed outputs → GEMM, weight grads into
+    sinks) vs fp32 autograd of w2(silu(x w1^T) * (x w3^T))."""
+    from fault_tolerant_llm_training_amd.ops import functional as Fx
+    from fault_tolerant_llm_training_amd.ops.grad_sink import GradSink
+
+    monkeypatch.setattr(Fx, "_DW_MODE", mode)
+    torch.manual_seed(5)
+    T, D, Fh = 256, 192, 320
+    x = torch.randn(T, D, device="cuda").bfloat16().requires_grad_(True)
+    w13 = (0.05 * torch.randn(2 * Fh, D, device="cuda")).bfloat16()
+    w2 = (0.05 * torch.randn(D, Fh, device="cuda")).bfloat16()
+    g13 = torch.empty(w13.numel(), dtype=torch.bfloat16, device="cuda")
+    g2 = torch.empty(w2.numel(), dtype=torch.bfloat16, device="cuda")
+    y = Fx.feed_forward(x, w13, w2, GradSink(g13), GradSink(g2))
+    dy = torch.randn(T, D, device="cuda").bfloat16()
+    y.backward(dy)
+    xr, w13r, w2r = (t.detach().float().requires_grad_(True) for t in (x, w13, w2))
+    g, u = (xr @ w13r.t()).chunk(2, -1)
+    yr = (F.silu(g) * u) @ w2r.t()
+    yr.backward(dy.float())
+    assert rel(y, yr) < 2e-2
+    assert rel(x.grad, xr.grad) < 2e-2
+    assert rel(g13.view(2 * Fh, D), w13r.grad) < 2e-2
+    assert rel(g2.view(D, Fh), w2r.grad) < 2e-2
