@@ -17,6 +17,17 @@ static torch::Tensor pinned_empty(uint64_t nbytes) {
       torch::TensorOptions().dtype(torch::kUInt8).device(torch::kCPU));
 }
 
+// A stream whose kernels may only be dispatched to the CUs set in `mask` (bit i = CU i,
+// 32 CUs per word). Returned as a raw handle for torch.cuda.ExternalStream; lives for the
+// process. Used to give memory-bound optimizer kernels a fixed CU share beside GEMMs.
+static uint64_t cu_mask_stream(int device, const std::vector<uint32_t>& mask) {
+  if (hipSetDevice(device) != hipSuccess) throw std::runtime_error("hipSetDevice failed");
+  hipStream_t s = nullptr;
+  hipError_t e = hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data());
+  if (e != hipSuccess) throw std::runtime_error(std::string("hipExtStreamCreateWithCUMask: ") + hipGetErrorString(e));
+  return reinterpret_cast<uint64_t>(s);
+}
+
 PYBIND11_MODULE(_runtime, m) {
   m.doc() = "Native fault-tolerance runtime: signal flags, snapshot engine, zip checkpoint writer";
 
@@ -71,5 +82,6 @@ PYBIND11_MODULE(_runtime, m) {
         py::call_guard<py::gil_scoped_release>(),
         "Sharded save: CRC + pwrite this rank's pieces into an existing file; returns per-piece CRC32s");
   m.def("crc32_combine", &crc32_combine_u32);
+  m.def("cu_mask_stream", &cu_mask_stream, py::arg("device"), py::arg("mask"));
   m.def("pinned_empty", &pinned_empty, "Exact-size pinned host buffer (hipHostMalloc) as a uint8 tensor");
 }
