@@ -188,6 +188,10 @@ class FlatAdamW(torch.optim.Optimizer):
             self._host_stats.copy_(self.stats)
         self._stats_step = self.step_count
 
+    def norm_for_logging(self):
+        """(device tensor holding the last step's pre-clip grad norm, event after which it is valid)."""
+        return self.stats[:1], self._stats_event
+
     def check_finite(self, block: bool = False) -> Optional[float]:
         """Deferred non-finite check of the last step's gradient norm.
 

@@ -81,15 +81,21 @@ class _LossLog:
         """Timing origin (call once the first step is enqueued)."""
         self.last = None
 
-    def push(self, step: int, loss: torch.Tensor, extra: Dict[str, Any]):
+    def push(self, step: int, loss: torch.Tensor, extra: Dict[str, Any], norm=None):
+        """``norm``: optional (device tensor, event) of the step's gradient norm (logged as grad_norm)."""
+        vals = [loss.detach().float().reshape(1)]
+        if norm is not None:
+            if self.cuda and norm[1] is not None:
+                torch.cuda.current_stream().wait_event(norm[1])  # the norm is finished on the optimizer stream
+            vals.append(norm[0].detach().float().reshape(1))
         if self.cuda:
-            h = torch.empty(1, dtype=torch.float32, pin_memory=True)
-            h.copy_(loss.detach().float().reshape(1), non_blocking=True)
+            h = torch.empty(len(vals), dtype=torch.float32, pin_memory=True)
+            h.copy_(torch.cat(vals), non_blocking=True)
             ev = torch.cuda.Event(enable_timing=True)
             ev.record()
             self.pending.append((step, h, ev, extra))
         else:
-            self.pending.append((step, loss.detach().float().reshape(1), time.perf_counter(), extra))
+            self.pending.append((step, torch.cat(vals), time.perf_counter(), extra))
 
     def flush(self, force: bool = False):
         keep = []
@@ -99,7 +105,11 @@ class _LossLog:
                 continue
             if self.cuda:
                 ev.synchronize()
-            msg = f"Training step: {step} | Loss: {h.item():.2f}"
+            hv = h.tolist()
+            msg = f"Training step: {step} | Loss: {hv[0]:.2f}"
+            if len(hv) > 1:
+                extra = dict(extra)
+                extra["grad_norm"] = f"{hv[1]:.3f}"
             if self.last is not None:
                 ls, lev = self.last
                 dt = (lev.elapsed_time(ev) / 1e3) if self.cuda else (ev - lev)
@@ -337,7 +347,7 @@ def train(args) -> int:
                 extra = {"lr": f"{lr_now:.3e}"}
                 if device.type == "cuda":
                     extra["peak_HBM_GB"] = f"{torch.cuda.max_memory_allocated(device) / 2**30:.1f}"
-                losslog.push(training_step, loss, extra)
+                losslog.push(training_step, loss, extra, norm=optimizer.norm_for_logging())
                 if metrics_f is not None:
                     now = time.perf_counter()
                     dt = (now - t_window) / max(1, steps_window)
