@@ -143,6 +143,10 @@ __device__ __forceinline__ f32x16_t mfma32(bf16x8_t a, bf16x8_t b, f32x16_t c) {
 // call) that softmax does not need — its arguments are <= 0 and tiny results flush to 0.
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
+// lse2 / delta rows are padded to a multiple of 32 queries, so a 32-query slice's
+// statistics are whole, aligned float4s (padding entries are never used unmasked).
+__host__ __device__ __forceinline__ int stat_stride(int S) { return (S + 31) & ~31; }
+
 __device__ __forceinline__ void map_head(int hh, int Hq, int Hkv, int& h, int& kvh) {
   // hh in [0, Hq) -> (h, kvh) so that the Hq/Hkv siblings of one KV head are
   // Hkv block-ids apart (same XCD when Hkv == 8).
@@ -332,7 +336,7 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(const bf16_t* __restr
         v.y = pack2(o[db][4 * g + 2] * inv, o[db][4 * g + 3] * inv);
         *reinterpret_cast<uint2*>(orow + db * 32 + 8 * g + 4 * hi) = v;
       }
-    if (hi == 0) lse2[((long)b * Hq + h) * S + qrow] = m + log2f(l);
+    if (hi == 0) lse2[((long)b * Hq + h) * stat_stride(S) + qrow] = m + log2f(l);
   }
 }
 
@@ -364,7 +368,7 @@ __global__ __launch_bounds__(256) void flash_bwd_pre_kernel(const bf16_t* __rest
     const long t = row / Hq;  // token = b*S + q
     const int h = (int)(row % Hq);
     const long bb = t / S, q = t % S;
-    delta[(bb * Hq + h) * S + q] = acc;
+    delta[(bb * Hq + h) * stat_stride(S) + q] = acc;
   }
 }
 
@@ -380,12 +384,14 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_kernel(
   constexpr int KIMG = BK * D * 2;   // K image (keys x D)
   constexpr int QIMG = BQ * D * 2;   // one Q or dO slice
   constexpr int DSIMG = BK * BQ * 2; // dS image [keys][32 q]
-  __shared__ __attribute__((aligned(16))) char smem[KIMG + 4 * QIMG + DSIMG + 4 * BQ * 4];
-  char* kimg = smem;
-  char* qimg = smem + KIMG;                 // [2][QIMG]
-  char* doimg = qimg + 2 * QIMG;            // [2][QIMG]
-  char* dsimg = doimg + 2 * QIMG;
-  float* stat = reinterpret_cast<float*>(dsimg + DSIMG);  // [2][lse 32 | delta 32]
+  // The two Q|dO slice buffers are separate LDS objects and the slice loop is unrolled
+  // by two, so every LDS read names a buffer the in-flight DMA provably does not write:
+  // the compiler then does not drain the prefetch (vmcnt(0)) before reading a slice.
+  __shared__ __attribute__((aligned(16))) char kds[KIMG + DSIMG];
+  __shared__ __attribute__((aligned(16))) char qdb0[2 * QIMG];  // [Q | dO], buffer 0
+  __shared__ __attribute__((aligned(16))) char qdb1[2 * QIMG];  // [Q | dO], buffer 1
+  char* kimg = kds;
+  char* dsimg = kds + KIMG;
 
   const int per = B * Hq;
   const int L = blockIdx.x;
@@ -403,31 +409,41 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_kernel(
   const bf16_t* Kg = qk + (long)b * S * ldqk + (long)(Hq + kvh) * D;
   const bf16_t* Vg = qkv + (long)b * S * ldv + (long)(Hq + Hkv + kvh) * D;
   const bf16_t* dOg = dO + (long)b * S * ldo + (long)h * D;
-  const float* lseg = lse2 + ((long)b * Hq + h) * S;
-  const float* delg = delta + ((long)b * Hq + h) * S;
+  const float* lseg = lse2 + ((long)b * Hq + h) * stat_stride(S);
+  const float* delg = delta + ((long)b * Hq + h) * stat_stride(S);
 
-  // K tile -> LDS (all 128 keys), V fragments of this wave's 32 keys -> VGPRs
+  // K and V fragments of this wave's 32 keys -> VGPRs (the S = Q K^T and dP = dO V^T
+  // B operands, reused by every query slice); the in-kernel dQ stage (DQ != 1) also
+  // needs all 128 keys of K as an LDS image.
+  if constexpr (DQ != 1) {
 #pragma unroll
-  for (int i = 0; i < BK * DCH / 256; ++i) {
-    const int id = tid + i * 256, row = id / DCH, c = id % DCH;
-    const long key = min(kb0 + row, S - 1);
-    *reinterpret_cast<uint4*>(kimg + lds_off<D>(row, c)) =
-        *reinterpret_cast<const uint4*>(Kg + key * ldqk + c * 8);
+    for (int i = 0; i < BK * DCH / 256; ++i) {
+      const int id = tid + i * 256, row = id / DCH, c = id % DCH;
+      const long key = min(kb0 + row, S - 1);
+      *reinterpret_cast<uint4*>(kimg + lds_off<D>(row, c)) =
+          *reinterpret_cast<const uint4*>(Kg + key * ldqk + c * 8);
+    }
   }
-  bf16x8_t vf[KS];
+  bf16x8_t vf[KS], kf[KS];
   {
     const long key = min(kw + l32, S - 1);
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks)
+    for (int ks = 0; ks < KS; ++ks) {
       vf[ks] = *reinterpret_cast<const bf16x8_t*>(Vg + key * ldv + ks * 16 + hi * 8);
+      kf[ks] = *reinterpret_cast<const bf16x8_t*>(Kg + key * ldqk + ks * 16 + hi * 8);
+    }
   }
 
   const int qs0 = kb0 / BQ;
   const int nqs = (S + BQ - 1) / BQ;
-  float4 st = make_float4(0.f, 0.f, 0.f, 0.f);
   // Q / dO slices go global -> LDS by LDS-DMA: the swizzle is applied to the
   // per-lane SOURCE address (the LDS side is lane-linear), no staging VGPRs.
+  // The slice's lse / delta (query rows 8g + 4hi + 0..3 of the C layout) go straight
+  // to registers, one slice ahead: plain loads whose first use is behind the
+  // iteration's closing barrier (an LDS copy of them would make the compiler drain
+  // the in-flight DMA before reading it).
   constexpr int GPW = QIMG / 1024 / 4;  // glds instructions per wave per image
+  float4 lsn[4], dln[4];
 #define BWD_GLDS(QS, BUF)                                                      \
   {                                                                            \
     static_for<GPW>([&](auto I) {                                              \
@@ -435,24 +451,18 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_kernel(
       int r, c;                                                                \
       lds_inv<D>(piece * 64 + lane, r, c);                                     \
       const long q = min((QS) * BQ + r, S - 1);                                \
-      glds16(Qg + q * ldqk + c * 8, qimg + (BUF) * QIMG + piece * 1024);       \
-      glds16(dOg + q * ldo + c * 8, doimg + (BUF) * QIMG + piece * 1024);      \
+      char* qd_ = (BUF) ? qdb1 : qdb0;                                         \
+      glds16(Qg + q * ldqk + c * 8, qd_ + piece * 1024);                       \
+      glds16(dOg + q * ldo + c * 8, qd_ + QIMG + piece * 1024);                \
     });                                                                        \
-    if (tid < 16) {                                                            \
-      const int q = (QS) * BQ + (tid & 7) * 4;                                 \
-      const float* src = (tid < 8) ? lseg : delg;                              \
-      st.x = q + 0 < S ? src[q + 0] : 0.f;                                     \
-      st.y = q + 1 < S ? src[q + 1] : 0.f;                                     \
-      st.z = q + 2 < S ? src[q + 2] : 0.f;                                     \
-      st.w = q + 3 < S ? src[q + 3] : 0.f;                                     \
-    }                                                                          \
+    static_for<4>([&](auto G) {                                                \
+      const int q = (QS) * BQ + 8 * G + 4 * hi;                                \
+      lsn[G] = *reinterpret_cast<const float4*>(lseg + q);                     \
+      dln[G] = *reinterpret_cast<const float4*>(delg + q);                     \
+    });                                                                        \
   }
-#define BWD_STAT(BUF)                                                          \
-  if (tid < 16)                                                                \
-    *reinterpret_cast<float4*>(stat + (BUF) * 64 + (tid < 8 ? 0 : 32) + (tid & 7) * 4) = st;
 
   BWD_GLDS(qs0, 0)
-  BWD_STAT(0)
   __syncthreads();
 
   f32x16_t dk[NDB], dv[NDB];
@@ -466,13 +476,20 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_kernel(
   const int qdb = wave % NDB, qkp = wave / NDB;
   const int key = kw + l32;
 
-  for (int qs = qs0; qs < nqs; ++qs) {
-    const int cur = (qs - qs0) & 1;
+  auto iter = [&](const int qs, auto CUR) {
+    constexpr int cur = decltype(CUR)::value;
     const bool more = qs + 1 < nqs;
-    const char* qi = qimg + cur * QIMG;
-    const char* di = doimg + cur * QIMG;
-    const float* ls = stat + cur * 64;
-    const float* dl = ls + 32;
+    // Prefetch the next slice into the other buffer before computing this one (its
+    // last readers finished behind the previous iteration's closing barrier), so the
+    // DMA's latency hides under this slice's MFMAs instead of stalling the barrier.
+    float4 lsc[4], dlc[4];
+    static_for<4>([&](auto G) {
+      lsc[G] = lsn[G];
+      dlc[G] = dln[G];
+    });
+    if (more) BWD_GLDS(qs + 1, cur ^ 1)
+    const char* qi = cur ? qdb1 : qdb0;
+    const char* di = qi + QIMG;
     const int qb = qs * BQ;
     const bool active = qb + BQ - 1 >= kw;  // wave-uniform
     auto slice = [&](auto MASKED) {
@@ -482,28 +499,30 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_kernel(
       for (int r = 0; r < 16; ++r) s[r] = dp[r] = 0.f;
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
-        s = mfma32(ld_row<D>(qi, l32, 2 * ks + hi), ld_row<D>(kimg, wave * 32 + l32, 2 * ks + hi), s);
+        s = mfma32(ld_row<D>(qi, l32, 2 * ks + hi), kf[ks], s);
         dp = mfma32(ld_row<D>(di, l32, 2 * ks + hi), vf[ks], dp);
       }
       // C layout: lane -> key (col), registers -> query rows
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const float4 lq = *reinterpret_cast<const float4*>(ls + 8 * g + 4 * hi);
-        const float4 dq = *reinterpret_cast<const float4*>(dl + 8 * g + 4 * hi);
-        const float lv[4] = {lq.x, lq.y, lq.z, lq.w};
-        const float dv4[4] = {dq.x, dq.y, dq.z, dq.w};
+      static_for<4>([&](auto G) {
+        constexpr int g = G;
+        const float lv[4] = {lsc[g].x, lsc[g].y, lsc[g].z, lsc[g].w};
+        const float dv4[4] = {dlc[g].x, dlc[g].y, dlc[g].z, dlc[g].w};
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
           const int r = 4 * g + t;
           float p = fast_exp2(fmaf(s[r], sl2, -lv[t]));
+          float ds = p * (dp[r] - dv4[t]);
           if constexpr (MASK) {
+            // also covers padded rows q >= S, whose lse / delta are uninitialised
             const int q = qb + 8 * g + 4 * hi + t;
-            if (key > q || q >= S) p = 0.f;
+            const bool off = key > q || q >= S;
+            p = off ? 0.f : p;
+            ds = off ? 0.f : ds;
           }
-          dp[r] = p * (dp[r] - dv4[t]);
+          dp[r] = ds;
           s[r] = p;
         }
-      }
+      });
       const bf16x8_t pa[2] = {cvt8<0>(s), cvt8<8>(s)};
       const bf16x8_t da[2] = {cvt8<0>(dp), cvt8<8>(dp)};
 #pragma unroll
@@ -536,10 +555,9 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_kernel(
 #pragma unroll
       for (int g = 0; g < 4; ++g) *reinterpret_cast<uint2*>(row + (8 * g + 4 * hi) * 2) = make_uint2(0, 0);
     }
-    __syncthreads();
-    if (more) BWD_GLDS(qs + 1, cur ^ 1)
     // dQ[q, d] += scale * sum_keys dS[q, key] K[key, d]
     if constexpr (DQ != 1) {
+      __syncthreads();
       f32x16_t acc;
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[r] = 0.f;
@@ -563,11 +581,13 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_kernel(
         }
       }
     }
-    if (more) BWD_STAT(cur ^ 1)
     __syncthreads();
+  };
+  for (int qs = qs0; qs < nqs; qs += 2) {
+    iter(qs, std::integral_constant<int, 0>{});
+    if (qs + 1 < nqs) iter(qs + 1, std::integral_constant<int, 1>{});
   }
 #undef BWD_GLDS
-#undef BWD_STAT
 
   // dK / dV partials of this q-head (C layout: lane -> d, registers -> keys)
 #pragma unroll
@@ -626,8 +646,8 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dq_kernel(
     qf[ks] = *reinterpret_cast<const bf16x8_t*>(Qg + qr * ldqk + ks * 16 + hi * 8);
     df[ks] = *reinterpret_cast<const bf16x8_t*>(dOg + qr * ldo + ks * 16 + hi * 8);
   }
-  const float lq = lse2[((long)b * Hq + h) * S + qr];
-  const float dlq = delta[((long)b * Hq + h) * S + qr];
+  const float lq = lse2[((long)b * Hq + h) * stat_stride(S) + qr];
+  const float dlq = delta[((long)b * Hq + h) * stat_stride(S) + qr];
 
   const int kend = min((qt + 1) * BM, S);
   const int ntiles = (kend + BN - 1) / BN;
@@ -792,8 +812,9 @@ void check_inputs(const at::Tensor& qk, const at::Tensor& qkv, int64_t S, int64_
 
 }  // namespace
 
-// Returns (o [T, Hq*D] bf16, lse2 [B, Hq, S] fp32; lse2 = log2 of the softmax denominator
-// in the exp2 domain, i.e. P = exp2(s * scale * log2e - lse2)).
+// Returns (o [T, Hq*D] bf16, lse2 [B, Hq, Sp] fp32 with Sp = S rounded up to 32 (entries
+// >= S unused); lse2 = log2 of the softmax denominator in the exp2 domain, i.e.
+// P = exp2(s * scale * log2e - lse2)).
 std::tuple<at::Tensor, at::Tensor> flash_fwd(const at::Tensor& qk, const at::Tensor& qkv,
                                              int64_t S, int64_t Hq, int64_t Hkv, int64_t D) {
   check_inputs(qk, qkv, S, Hq, Hkv, D);
@@ -801,7 +822,7 @@ std::tuple<at::Tensor, at::Tensor> flash_fwd(const at::Tensor& qk, const at::Ten
   const int B = T / S;
   const at::DeviceGuard guard(qk.device());
   auto out = at::empty({T, Hq * D}, qk.options());
-  auto lse = at::empty({B, Hq, S}, qk.options().dtype(at::kFloat));
+  auto lse = at::empty({B, Hq, (long)stat_stride(S)}, qk.options().dtype(at::kFloat));
   const float sl2 = LOG2E_F / std::sqrt((float)D);
   const int nqt = (S + 127) / 128;
   dim3 grid(nqt * B * Hq), block(256);
@@ -827,10 +848,10 @@ at::Tensor flash_bwd(const at::Tensor& dout, const at::Tensor& qk, const at::Ten
   const int T = qk.size(0);
   const int B = T / S;
   TORCH_CHECK(dout.numel() == (long)T * Hq * D && out.numel() == (long)T * Hq * D, "flash_bwd: o shape");
-  TORCH_CHECK(lse.numel() == (long)B * Hq * S, "flash_bwd: lse shape");
+  TORCH_CHECK(lse.numel() == (long)B * Hq * stat_stride(S), "flash_bwd: lse shape");
   const at::DeviceGuard guard(qk.device());
   auto f32 = qk.options().dtype(at::kFloat);
-  auto delta = at::empty({B, Hq, S}, f32);
+  auto delta = at::empty({B, Hq, (long)stat_stride(S)}, f32);
   // mode 0: dQ by fp32 atomics in the KV-major kernel (fastest);
   // mode 1: deterministic — KV kernel without dQ + Q-major dQ kernel (no atomics);
   // mode 2: timing experiment only (racy dQ stores).
