@@ -236,6 +236,9 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(const bf16_t* __restr
 #pragma unroll
     for (int r = 0; r < 16; ++r) o[db][r] = 0.f;
   float m = -INFINITY, l = 0.f;
+  // Materialise the Q fragments before the loop: left pending, the compiler's waits for
+  // them inside the loop would also drain the next tile's prefetch (in-order vmcnt).
+  static_for<KS>([&qf](auto I) { asm volatile("" ::"v"(__builtin_bit_cast(u32x4, qf[I]))); });
 
   for (int kt = 0; kt < ntiles; ++kt) {
     const int cur = kt & 1;
@@ -676,6 +679,12 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dq_kernel(
   DQ_GLOAD(0)
   DQ_SWRITE(0)
   __syncthreads();
+  // Materialise the Q / dO fragments and row statistics before the loop: left pending,
+  // the compiler's waits for them inside the loop would drain the next tile's prefetch.
+  asm volatile("" ::"v"(lq), "v"(dlq));
+  static_for<KS>([&qf, &df](auto I) {
+    asm volatile("" ::"v"(__builtin_bit_cast(u32x4, qf[I])), "v"(__builtin_bit_cast(u32x4, df[I])));
+  });
 
   f32x16_t dq[NDB];
 #pragma unroll
