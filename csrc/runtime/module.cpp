@@ -82,6 +82,13 @@ PYBIND11_MODULE(_runtime, m) {
         py::call_guard<py::gil_scoped_release>(),
         "Sharded save: CRC + pwrite this rank's pieces into an existing file; returns per-piece CRC32s");
   m.def("crc32_combine", &crc32_combine_u32);
+  py::class_<FileReader>(m, "FileReader")
+      .def(py::init<const std::string&, int, bool>(), py::arg("path"), py::arg("threads") = 8,
+           py::arg("direct") = true)
+      .def("read", &FileReader::read, py::arg("offset"), py::arg("ptr"), py::arg("nbytes"),
+           py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("bytes", &FileReader::bytes)
+      .def_property_readonly("direct_bytes", &FileReader::direct_bytes);
   m.def("cu_mask_stream", &cu_mask_stream, py::arg("device"), py::arg("mask"));
   m.def("pinned_empty", &pinned_empty, "Exact-size pinned host buffer (hipHostMalloc) as a uint8 tensor");
 }

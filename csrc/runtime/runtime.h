@@ -108,6 +108,24 @@ class ZipWriter {
   ZipStats stats_;
 };
 
+// ---- file_reader.cpp -------------------------------------------------------------
+// Parallel pread (O_DIRECT for 4 KiB-aligned bodies) of a file range into host memory:
+// the checkpoint restore path (file -> pinned chunk -> HBM), see ckpt/restore.py.
+class FileReader {
+ public:
+  FileReader(const std::string& path, int nthreads, bool direct);
+  ~FileReader();
+  void read(uint64_t off, uintptr_t ptr, uint64_t len);
+  uint64_t bytes() const { return bytes_; }
+  uint64_t direct_bytes() const { return direct_bytes_; }
+
+ private:
+  std::string path_;
+  int nthreads_;
+  int fd_ = -1, dfd_ = -1;
+  uint64_t bytes_ = 0, direct_bytes_ = 0;
+};
+
 // ---- snapshot.cpp (HIP) ------------------------------------------------------------
 // Side-stream copy engine: D2D snapshot into reserved HBM and D2H drain into
 // pinned host memory, ordered after the compute stream by events.

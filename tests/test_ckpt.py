@@ -139,3 +139,38 @@ def test_failed_publish_raises_and_leaves_no_partial_file(tmp_path):
     ok = str(tmp_path / "f.ckpt")
     eng.save(ok, lambda host: build_checkpoint(m, opt, s, 2, host), blocking=True)
     assert load_checkpoint(ok)["training_step"] == 2
+
+
+def test_file_reader_ranges(tmp_path):
+    """Native parallel pread (O_DIRECT bodies + buffered head/tail) returns the file's bytes."""
+    from fault_tolerant_llm_training_amd._native import runtime
+
+    data = torch.randint(0, 256, (3 * (1 << 20) + 12345,), dtype=torch.uint8)
+    p = tmp_path / "blob.bin"
+    p.write_bytes(data.numpy().tobytes())
+    r = runtime().FileReader(str(p), 4, True)
+    for off, n in ((0, data.numel()), (4096, 1 << 20), (8192, 12345), (77, 5000), (1 << 20, 2 * (1 << 20) + 12345)):
+        out = torch.empty(n, dtype=torch.uint8)
+        r.read(off, out.data_ptr(), n)
+        assert torch.equal(out, data[off : off + n]), (off, n)
+    assert r.bytes > 0
+    with pytest.raises(RuntimeError):
+        out = torch.empty(100, dtype=torch.uint8)
+        r.read(data.numel() - 10, out.data_ptr(), 100)  # past the end of the file
+
+
+def test_file_backing_of_mmap_checkpoint(tmp_path):
+    """A tensor of torch.load(mmap=True) maps the checkpoint file; the reported offset holds its bytes."""
+    from fault_tolerant_llm_training_amd.ckpt.restore import file_backing
+
+    t = torch.randn(1 << 18)
+    p = tmp_path / "ck.pt"
+    torch.save({"a": torch.arange(10), "t": t}, str(p))
+    sd = torch.load(str(p), mmap=True, weights_only=True)
+    fb = file_backing(sd["t"])
+    assert fb is not None and os.path.samefile(fb[0], str(p))
+    with open(p, "rb") as f:
+        f.seek(fb[1])
+        raw = f.read(t.numel() * 4)
+    assert torch.equal(torch.frombuffer(bytearray(raw), dtype=torch.float32), t)
+    assert file_backing(torch.randn(100)) is None

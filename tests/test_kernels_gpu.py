@@ -289,3 +289,20 @@ def test_feed_forward_fused(mode, monkeypatch):
     assert rel(x.grad, xr.grad) < 2e-2
     assert rel(g13.view(2 * Fh, D), w13r.grad) < 2e-2
     assert rel(g2.view(D, Fh), w2r.grad) < 2e-2
+
+
+def test_h2d_from_checkpoint_file(tmp_path):
+    """Restore path for an mmap'd checkpoint tensor: file -> pinned ring (native pread) -> HBM."""
+    from fault_tolerant_llm_training_amd.ckpt import restore
+
+    src = torch.randn(150 * (1 << 20) // 2).bfloat16()  # 150 MiB, ragged last chunk
+    p = tmp_path / "ck.pt"
+    torch.save({"x": src}, str(p))
+    t = torch.load(str(p), mmap=True, weights_only=True)["x"]
+    before = restore.STATS["file_bytes"]
+    dst = torch.empty(src.numel(), dtype=torch.bfloat16, device="cuda")
+    restore.h2d(dst, t, min_bytes=0)
+    torch.cuda.synchronize()
+    assert restore.STATS["file_bytes"] - before == src.numel() * 2
+    assert torch.equal(dst.cpu(), src)
+    restore.release()
