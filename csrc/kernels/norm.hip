@@ -123,12 +123,15 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(
     const float mu = LN ? mean_in[row] : 0.f;
     const bf16_t* xr = x + (size_t)row * N;
     const bf16_t* dyr = dy + (size_t)row * N;
-    uint4 xv[CH], gv[CH];
+    const bf16_t* drr = dres ? dres + (size_t)row * N : nullptr;
+    // all three row loads are issued together (one HBM round trip per row, not two)
+    uint4 xv[CH], gv[CH], rv[CH];
 #pragma unroll
     for (int c = 0; c < CH; ++c) {
       const int idx = c * 512 + lane * 8;
       xv[c] = idx < N ? *reinterpret_cast<const uint4*>(xr + idx) : z;
       gv[c] = idx < N ? *reinterpret_cast<const uint4*>(dyr + idx) : z;
+      rv[c] = (drr && idx < N) ? *reinterpret_cast<const uint4*>(drr + idx) : z;
     }
     float sdn = 0.f, sdnn = 0.f;
 #pragma unroll
@@ -149,7 +152,6 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(
     sdnn = wave_sum(sdnn) * invN;
     if (LN) sdn = wave_sum(sdn) * invN;
     bf16_t* dxr = dx + (size_t)row * N;
-    const bf16_t* drr = dres ? dres + (size_t)row * N : nullptr;
 #pragma unroll
     for (int c = 0; c < CH; ++c) {
       const int idx = c * 512 + lane * 8;
@@ -165,7 +167,7 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(
         }
         if (drr) {
           float rr[8];
-          unpack8(*reinterpret_cast<const uint4*>(drr + idx), rr);
+          unpack8(rv[c], rr);
 #pragma unroll
           for (int j = 0; j < 8; ++j) o[j] += rr[j];
         }

@@ -17,36 +17,72 @@
 // ~8e9 elements instead of ~300-tensor foreach chains.
 #include "torch_utils.h"
 
+#include <cstdlib>
+
 namespace {
 
-template <typename T>
+// 16-B vector access; NT = non-temporal (streaming) loads/stores: every byte of the
+// optimizer pass is touched exactly once, so nothing is worth keeping in L2/MALL.
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+
+template <bool NT>
+__device__ __forceinline__ uint4 ld16(const void* p) {
+  if constexpr (NT) {
+    const u32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+  } else {
+    return *reinterpret_cast<const uint4*>(p);
+  }
+}
+
+template <bool NT>
+__device__ __forceinline__ void st16(void* p, uint4 v) {
+  if constexpr (NT) {
+    const u32x4_t w = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(w, reinterpret_cast<u32x4_t*>(p));
+  } else {
+    *reinterpret_cast<uint4*>(p) = v;
+  }
+}
+
+template <typename T, bool NT = false>
 struct V8;
-template <>
-struct V8<bf16_t> {
-  __device__ static void load(const bf16_t* p, float* f) { unpack8(*reinterpret_cast<const uint4*>(p), f); }
-  __device__ static void store(bf16_t* p, const float* f) { *reinterpret_cast<uint4*>(p) = pack8(f); }
+template <bool NT>
+struct V8<bf16_t, NT> {
+  __device__ static void load(const bf16_t* p, float* f) { unpack8(ld16<NT>(p), f); }
+  __device__ static void store(bf16_t* p, const float* f) { st16<NT>(p, pack8(f)); }
 };
-template <>
-struct V8<float> {
+template <bool NT>
+struct V8<float, NT> {
   __device__ static void load(const float* p, float* f) {
-    const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
-    f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w; f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
+    const uint4 a = ld16<NT>(p), b = ld16<NT>(p + 4);
+    f[0] = __uint_as_float(a.x); f[1] = __uint_as_float(a.y); f[2] = __uint_as_float(a.z); f[3] = __uint_as_float(a.w);
+    f[4] = __uint_as_float(b.x); f[5] = __uint_as_float(b.y); f[6] = __uint_as_float(b.z); f[7] = __uint_as_float(b.w);
   }
   __device__ static void store(float* p, const float* f) {
-    *reinterpret_cast<float4*>(p) = make_float4(f[0], f[1], f[2], f[3]);
-    *reinterpret_cast<float4*>(p + 4) = make_float4(f[4], f[5], f[6], f[7]);
+    st16<NT>(p, make_uint4(__float_as_uint(f[0]), __float_as_uint(f[1]), __float_as_uint(f[2]), __float_as_uint(f[3])));
+    st16<NT>(p + 4, make_uint4(__float_as_uint(f[4]), __float_as_uint(f[5]), __float_as_uint(f[6]), __float_as_uint(f[7])));
   }
 };
+
+// FT_STREAM_NT=0 selects plain loads/stores for the optimizer-pass kernels (A/B).
+bool stream_nt() {
+  static const bool nt = [] {
+    const char* e = std::getenv("FT_STREAM_NT");
+    return e == nullptr || std::atoi(e) != 0;
+  }();
+  return nt;
+}
 
 constexpr int NORM_BLOCKS = 2048;
 
-template <typename G>
+template <typename G, bool NT>
 __global__ __launch_bounds__(256) void sumsq_kernel(const G* __restrict__ g, long n8,
                                                     float* __restrict__ partial) {
   float s = 0.f;
   for (long i = blockIdx.x * 256L + threadIdx.x; i < n8; i += (long)gridDim.x * 256) {
     float x[8];
-    V8<G>::load(g + i * 8, x);
+    V8<G, NT>::load(g + i * 8, x);
 #pragma unroll
     for (int j = 0; j < 8; ++j) s += x[j] * x[j];
   }
@@ -86,7 +122,7 @@ __global__ __launch_bounds__(1024) void norm_finish_kernel(const float* __restri
   }
 }
 
-template <typename P, typename S>
+template <typename P, typename S, bool NT>
 __global__ __launch_bounds__(256) void adamw_kernel(P* __restrict__ p, const P* __restrict__ g,
                                                     S* __restrict__ m, S* __restrict__ v,
                                                     long n8, float lr, float beta1, float beta2,
@@ -99,10 +135,10 @@ __global__ __launch_bounds__(256) void adamw_kernel(P* __restrict__ p, const P* 
   const float step = lr * inv_bc1;
   for (long i = blockIdx.x * 256L + threadIdx.x; i < n8; i += (long)gridDim.x * 256) {
     float pf[8], gf[8], mf[8], vf[8];
-    V8<P>::load(p + i * 8, pf);
-    V8<P>::load(g + i * 8, gf);
-    V8<S>::load(m + i * 8, mf);
-    V8<S>::load(v + i * 8, vf);
+    V8<P, NT>::load(p + i * 8, pf);
+    V8<P, NT>::load(g + i * 8, gf);
+    V8<S, NT>::load(m + i * 8, mf);
+    V8<S, NT>::load(v + i * 8, vf);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const float gj = gf[j] * coef;
@@ -112,9 +148,9 @@ __global__ __launch_bounds__(256) void adamw_kernel(P* __restrict__ p, const P* 
       const float denom = sqrtf(vf[j]) * inv_sqrt_bc2 + eps;
       pf[j] -= step * mf[j] / denom;
     }
-    V8<P>::store(p + i * 8, pf);
-    V8<S>::store(m + i * 8, mf);
-    V8<S>::store(v + i * 8, vf);
+    V8<P, NT>::store(p + i * 8, pf);
+    V8<S, NT>::store(m + i * 8, mf);
+    V8<S, NT>::store(v + i * 8, vf);
   }
 }
 
@@ -124,6 +160,20 @@ __global__ __launch_bounds__(256) void adamw_kernel(P* __restrict__ p, const P* 
 int stream_grid(long n8) {
   long g = (n8 + 255) / 256;
   return (int)std::max(1L, std::min(g, 65535L));
+}
+
+void launch_sumsq(const at::Tensor& grad, long n8, int nb, float* partial) {
+  const bool nt = stream_nt();
+#define FT_SSQ(G, NT_) \
+  hipLaunchKernelGGL((sumsq_kernel<G, NT_>), dim3(nb), dim3(256), 0, ft_stream(), cptr<G>(grad), n8, partial)
+  if (grad.scalar_type() == at::kBFloat16) {
+    if (nt) FT_SSQ(bf16_t, true); else FT_SSQ(bf16_t, false);
+  } else if (grad.scalar_type() == at::kFloat) {
+    if (nt) FT_SSQ(float, true); else FT_SSQ(float, false);
+  } else {
+    TORCH_CHECK(false, "sumsq: unsupported dtype");
+  }
+#undef FT_SSQ
 }
 
 }  // namespace
@@ -138,14 +188,7 @@ void grad_norm_(const at::Tensor& grad, const at::Tensor& stats, double max_norm
   const long n8 = grad.numel() / 8;
   const int nb = std::max(1, std::min(NORM_BLOCKS, (int)((n8 + 255) / 256)));
   auto partial = at::empty({nb}, grad.options().dtype(at::kFloat));
-  if (grad.scalar_type() == at::kBFloat16)
-    hipLaunchKernelGGL(sumsq_kernel<bf16_t>, dim3(nb), dim3(256), 0, ft_stream(), cptr<bf16_t>(grad),
-                       n8, mptr<float>(partial));
-  else if (grad.scalar_type() == at::kFloat)
-    hipLaunchKernelGGL(sumsq_kernel<float>, dim3(nb), dim3(256), 0, ft_stream(), cptr<float>(grad),
-                       n8, mptr<float>(partial));
-  else
-    TORCH_CHECK(false, "grad_norm: unsupported dtype");
+  launch_sumsq(grad, n8, nb, mptr<float>(partial));
   FT_LAUNCH_CHECK();
   hipLaunchKernelGGL(norm_finish_kernel, dim3(1), dim3(1024), 0, ft_stream(), cptr<float>(partial), nb,
                      1.f, (float)max_norm, mptr<float>(stats));
@@ -177,10 +220,18 @@ void adamw_(const at::Tensor& p, const at::Tensor& g, const at::Tensor& m, const
   // the dispatcher can interleave a higher-priority stream's workgroups.
   if (max_blocks > 0) nb = (int)std::max(1L, std::min((n8 + 255) / 256, (long)max_blocks));
   const dim3 grid(nb), block(256);
-#define FT_ADAM(PT, ST)                                                                            \
-  hipLaunchKernelGGL((adamw_kernel<PT, ST>), grid, block, 0, ft_stream(), mptr<PT>(p), cptr<PT>(g), \
-                     mptr<ST>(m), mptr<ST>(v), n8, (float)lr, (float)beta1, (float)beta2,          \
-                     (float)eps, (float)wd, inv_bc1, inv_sqrt_bc2, cptr<float>(stats))
+  const bool nt = stream_nt();
+#define FT_ADAM(PT, ST)                                                                             \
+  do {                                                                                              \
+  if (nt)                                                                                           \
+    hipLaunchKernelGGL((adamw_kernel<PT, ST, true>), grid, block, 0, ft_stream(), mptr<PT>(p),       \
+                       cptr<PT>(g), mptr<ST>(m), mptr<ST>(v), n8, (float)lr, (float)beta1,          \
+                       (float)beta2, (float)eps, (float)wd, inv_bc1, inv_sqrt_bc2, cptr<float>(stats)); \
+  else                                                                                              \
+    hipLaunchKernelGGL((adamw_kernel<PT, ST, false>), grid, block, 0, ft_stream(), mptr<PT>(p),      \
+                       cptr<PT>(g), mptr<ST>(m), mptr<ST>(v), n8, (float)lr, (float)beta1,          \
+                       (float)beta2, (float)eps, (float)wd, inv_bc1, inv_sqrt_bc2, cptr<float>(stats)); \
+  } while (0)
   if (p.scalar_type() == at::kBFloat16 && m.scalar_type() == at::kBFloat16) FT_ADAM(bf16_t, bf16_t);
   else if (p.scalar_type() == at::kBFloat16 && m.scalar_type() == at::kFloat) FT_ADAM(bf16_t, float);
   else if (p.scalar_type() == at::kFloat && m.scalar_type() == at::kFloat) FT_ADAM(float, float);
@@ -202,14 +253,7 @@ void sumsq_into_(const at::Tensor& grad, const at::Tensor& partial) {
   const at::DeviceGuard guard(grad.device());
   const long n8 = grad.numel() / 8;
   const int nb = (int)partial.numel();
-  if (grad.scalar_type() == at::kBFloat16)
-    hipLaunchKernelGGL(sumsq_kernel<bf16_t>, dim3(nb), dim3(256), 0, ft_stream(), cptr<bf16_t>(grad),
-                       n8, mptr<float>(partial));
-  else if (grad.scalar_type() == at::kFloat)
-    hipLaunchKernelGGL(sumsq_kernel<float>, dim3(nb), dim3(256), 0, ft_stream(), cptr<float>(grad),
-                       n8, mptr<float>(partial));
-  else
-    TORCH_CHECK(false, "sumsq_into: unsupported dtype");
+  launch_sumsq(grad, n8, nb, mptr<float>(partial));
   FT_LAUNCH_CHECK();
 }
 

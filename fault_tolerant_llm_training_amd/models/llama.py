@@ -272,6 +272,10 @@ class Transformer(nn.Module):
 
 
 def build_model(args: TransformerModelArgs, device, dtype=torch.bfloat16, seed: int = 1234) -> Transformer:
+    if torch.device(device).type == "cuda":
+        from ..ops.gemm_tuning import use_tuned_gemms
+
+        use_tuned_gemms()  # per-shape hipBLASLt/rocBLAS solutions (tuning/gemm_gfx950.csv), if present
     return Transformer(args).materialize(device, dtype, seed)
 
 

@@ -69,6 +69,64 @@ def weight_grad(dy2: torch.Tensor, x2: torch.Tensor, sink: Optional[GradSink],
     return torch.mm(dy2.t(), x2)
 
 
+# Weight-gradient GEMMs on a side stream (FT_DW_STREAM=1): dW and the dX GEMM of the same
+# node are independent, and the small projections (wo, wqkv: 128-192 output tiles of
+# 256x256) leave half of the 256 CUs idle when run one after the other. The side stream
+# waits for the compute stream before each dW (so it sees dY / X), the operands are
+# recorded on it (the caching allocator keeps them alive), and the bucket hooks fired
+# from it order the reducer's collectives after it. join_dw_stream() (GradReducer.finish,
+# FlatAdamW.step) makes the compute stream wait for every dW before the optimizer.
+_DW_STREAM = os.environ.get("FT_DW_STREAM", "0") == "1"
+_dw_streams = {}
+
+
+def set_dw_stream(on: bool) -> None:
+    global _DW_STREAM
+    _DW_STREAM = bool(on)
+
+
+def _dev_key(dev: torch.device) -> int:
+    return dev.index if dev.index is not None else torch.cuda.current_device()
+
+
+def _dw_side(dev: torch.device) -> torch.cuda.Stream:
+    k = _dev_key(dev)
+    s = _dw_streams.get(k)
+    if s is None:
+        s = _dw_streams[k] = torch.cuda.Stream(device=k)
+    return s
+
+
+def weight_grad_async(dy2: torch.Tensor, x2: Optional[torch.Tensor], sink: Optional[GradSink],
+                      dyT: Optional[torch.Tensor] = None, xT: Optional[torch.Tensor] = None):
+    """:func:`weight_grad` into ``sink`` on the dW side stream (or inline when disabled)."""
+    if not (_DW_STREAM and dy2.is_cuda and sink is not None):
+        return weight_grad(dy2, x2, sink, dyT, xT)
+    cur = torch.cuda.current_stream(dy2.device)
+    side = _dw_side(dy2.device)
+    side.wait_stream(cur)
+    with torch.cuda.stream(side):
+        weight_grad(dy2, x2, sink, dyT, xT)
+    for t in (dy2, x2, dyT, xT):
+        if t is not None:
+            t.record_stream(side)
+    return None
+
+
+def active_dw_stream(dev: torch.device) -> Optional[torch.cuda.Stream]:
+    """The dW side stream of ``dev`` if weight gradients may be in flight on it, else None."""
+    return _dw_streams.get(_dev_key(dev)) if _DW_STREAM else None
+
+
+def join_dw_stream() -> None:
+    """Make the current stream wait for all weight gradients issued on the dW side stream."""
+    if _dw_streams:
+        cur = torch.cuda.current_stream()
+        s = _dw_streams.get(_dev_key(cur.device))
+        if s is not None:
+            cur.wait_stream(s)
+
+
 def _write_weight_grad(sink: Optional[GradSink], g: torch.Tensor):
     """CPU helper: route a computed weight gradient into its sink (or return it)."""
     if sink is None:
@@ -237,7 +295,7 @@ class LinearFn(torch.autograd.Function):
         dy2 = dy.reshape(-1, N)
         dw = None
         # weight gradient first, so its all-reduce bucket can launch while dx runs
-        dw = weight_grad(dy2, x2, ctx.sink)
+        dw = weight_grad_async(dy2, x2, ctx.sink)
         dx = torch.mm(dy2, w).view(ctx.xshape)
         return dx, dw, None, (dy if ctx.has_res else None)
 
@@ -380,16 +438,16 @@ class FeedForwardFn(torch.autograd.Function):
         K_ = kernels()
         dy2 = dy.reshape(-1, w2.shape[0]).contiguous()
         if ctx.tn:
-            dw2 = weight_grad(dy2, None, sink2, xT=a_or_T)
+            dw2 = weight_grad_async(dy2, None, sink2, xT=a_or_T)
         else:
-            dw2 = weight_grad(dy2, a_or_T, sink2)
+            dw2 = weight_grad_async(dy2, a_or_T, sink2)
         da = torch.mm(dy2, w2)
         if ctx.tn:
             dgu, dguT = K_.swiglu_bwd_t(da, gu)
         else:
             dgu, dguT = K_.swiglu_bwd(da, gu), None
         del da
-        dw13 = weight_grad(dgu, x2, sink13, dyT=dguT)
+        dw13 = weight_grad_async(dgu, x2, sink13, dyT=dguT)
         dx = torch.mm(dgu, w13).view(ctx.xshape)
         return dx, dw13, dw2, None, None
 
@@ -431,7 +489,7 @@ class LMHeadCrossEntropyFn(torch.autograd.Function):
             gf = g.detach().float().reshape(1).contiguous()
             kernels().xent_bwd_(logits, lab, lse, gf, inv_count.float().reshape(1).contiguous(), IGNORE_INDEX)
             dlogits = logits  # overwritten in place
-            dw = weight_grad(dlogits, h2, sink)
+            dw = weight_grad_async(dlogits, h2, sink)
             dh = torch.mm(dlogits, w).view(ctx.hshape)
             return dh, dw, None, None, None
         h2, w, lab, inv_count = ctx.saved_tensors

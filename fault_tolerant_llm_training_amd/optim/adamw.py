@@ -146,6 +146,9 @@ class FlatAdamW(torch.optim.Optimizer):
         if r is None:
             # stand-alone: whole-buffer norm + one AdamW launch on the current stream
             if cuda:
+                from ..ops.functional import join_dw_stream
+
+                join_dw_stream()
                 kernels().grad_norm_(f.grads, self.stats, self.max_grad_norm)
             else:
                 _norm_reference(f.grads.float().pow(2).sum().reshape(1), self.stats, self.max_grad_norm)

@@ -215,6 +215,20 @@ class GradReducer:
             part[0] = g.float().pow(2).sum()
 
     def _launch(self, b: Bucket) -> None:
+        if self.cuda:
+            from ..ops.functional import active_dw_stream
+
+            dws = active_dw_stream(self.flat.device)
+            if dws is not None and dws != torch.cuda.current_stream():
+                # part of this bucket's gradients may still be running on the dW side stream:
+                # issue the bucket's work from that stream, after the compute stream's work
+                dws.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(dws):
+                    self._launch_now(b)
+                return
+        self._launch_now(b)
+
+    def _launch_now(self, b: Bucket) -> None:
         b.launched = True
         grads = self.flat.grads[b.lo : b.hi]
         if b.sparse:
@@ -240,6 +254,10 @@ class GradReducer:
     def finish(self) -> None:
         """Launch stragglers; after this, ``partials`` hold every bucket's sum of squares
         (on the side stream when overlapping, else synchronously)."""
+        if self.cuda:
+            from ..ops.functional import join_dw_stream
+
+            join_dw_stream()  # weight gradients still running on the dW side stream
         for b in self.buckets:
             if not b.launched:
                 self._launch(b)

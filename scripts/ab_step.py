@@ -1,0 +1,108 @@
+#!/usr/bin/env python3
+"""Same-process A/B of step-level knobs on the Llama-3-8B bench step (MI355X).
+
+Knobs toggled between timing windows (alternating rounds, so box and clock drift cancel):
+  gemm  — TunableOp GEMM solution table (tuning/gemm_gfx950.csv) vs the hipBLASLt heuristic
+  dw    — weight-gradient GEMMs on a side stream, concurrent with the dX GEMMs
+Usage: python scripts/ab_step.py [--steps 8] [--rounds 3] [--configs gemm,dw ...]
+"""
+from __future__ import annotations
+
+import argparse
+import itertools
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="llama3-8b")
+    ap.add_argument("--seq-len", type=int, default=2048)
+    ap.add_argument("--vocab-size", type=int, default=131072)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=8)
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--knobs", default="gemm,dw")
+    a = ap.parse_args()
+
+    from fault_tolerant_llm_training_amd.data.synthetic import SyntheticTokens
+    from fault_tolerant_llm_training_amd.models.llama import build_model, model_args_for
+    from fault_tolerant_llm_training_amd.ops import functional as Fx
+    from fault_tolerant_llm_training_amd.ops import gemm_tuning
+    from fault_tolerant_llm_training_amd.optim.adamw import FlatAdamW
+    from fault_tolerant_llm_training_amd.parallel.ddp import GradReducer
+    from fault_tolerant_llm_training_amd.utils.lr import build_lr_scheduler
+
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    margs = model_args_for(a.model, vocab_size=a.vocab_size, seq_len=a.seq_len)
+    model = build_model(margs, dev, torch.bfloat16, seed=1234)
+    print(f"[ab] tuned GEMM table loaded: {gemm_tuning.use_tuned_gemms()}", flush=True)
+    red = GradReducer(model.flat, model.sinks_in_backward_order(), bucket_mb=256.0)
+    opt = FlatAdamW(model.parameters(), model.flat, lr=5e-5, max_grad_norm=1.0, reducer=red)
+    model.gate = opt.gate
+    sched = build_lr_scheduler(opt, 100)
+    data = SyntheticTokens(a.vocab_size, a.seq_len, seed=4321)
+    inv = torch.full((1,), 1.0 / a.seq_len, dtype=torch.float32, device=dev)
+    it = [0]
+
+    def step():
+        tok, lab = data.batch(it[0], 1)
+        it[0] += 1
+        loss = model(tok.to(dev, non_blocking=True), lab.to(dev, non_blocking=True), inv)
+        loss.backward()
+        red.finish()
+        opt.clip_grad_norm_(1.0)
+        opt.step()
+        sched.step()
+        return loss
+
+    def window(n):
+        opt.gate.wait_all()
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for _ in range(n):
+            step()
+        opt.gate.wait_all()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t) / n * 1e3
+
+    knobs = [k for k in a.knobs.split(",") if k]
+    setters = {"gemm": gemm_tuning.set_enabled, "dw": Fx.set_dw_stream}
+    configs = list(itertools.product([False, True], repeat=len(knobs)))
+
+    def apply(cfg):
+        for k, on in zip(knobs, cfg):
+            setters[k](on)
+
+    for cfg in configs:  # warm every configuration (allocator pools, side streams)
+        apply(cfg)
+        for _ in range(a.warmup):
+            step()
+    res = {cfg: [] for cfg in configs}
+    for r in range(a.rounds):
+        for cfg in configs:
+            apply(cfg)
+            ms = window(a.steps)
+            res[cfg].append(ms)
+            name = " ".join(f"{k}={'on' if on else 'off'}" for k, on in zip(knobs, cfg))
+            print(f"[ab] round {r} {name}: {ms:.2f} ms/step", flush=True)
+    base = min(res[configs[0]])
+    for cfg in configs:
+        name = " ".join(f"{k}={'on' if on else 'off'}" for k, on in zip(knobs, cfg))
+        best = min(res[cfg])
+        print(f"[ab] {name:24s} best {best:7.2f} ms/step  median {sorted(res[cfg])[len(res[cfg]) // 2]:7.2f}  "
+              f"{base / best:.3f}x vs all-off  ({2048 * 1000 / best:.0f} tok/s)", flush=True)
+    loss = step()
+    torch.cuda.synchronize()
+    print(f"[ab] final loss {float(loss):.4f}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
