@@ -77,7 +77,7 @@ __global__ __launch_bounds__(256) void swiglu_fwd_t_kernel(const bf16_t* __restr
 #pragma unroll
     for (int j = 0; j < 8; ++j) o[j] = g[j] * sigmoidf_(g[j]) * u[j];
     const uint4 v = pack8(o);
-    *reinterpret_cast<uint4*>(a + (long)(r0 + row) * F + c0 + seg * 8) = v;
+    if (a != nullptr) *reinterpret_cast<uint4*>(a + (long)(r0 + row) * F + c0 + seg * 8) = v;
     const bf16_t* e = reinterpret_cast<const bf16_t*>(&v);
 #pragma unroll
     for (int j = 0; j < 8; ++j) tile[row][seg * 8 + j] = e[j];
@@ -118,8 +118,10 @@ __global__ __launch_bounds__(256) void swiglu_bwd_t_kernel(const bf16_t* __restr
       dg[j] = d[j] * u[j] * (s + silu * (1.f - s));
     }
     const uint4 vg = pack8(dg), vu = pack8(du);
-    *reinterpret_cast<uint4*>(dgu + base) = vg;
-    *reinterpret_cast<uint4*>(dgu + base + F) = vu;
+    if (dgu != nullptr) {
+      *reinterpret_cast<uint4*>(dgu + base) = vg;
+      *reinterpret_cast<uint4*>(dgu + base + F) = vu;
+    }
     const bf16_t* eg = reinterpret_cast<const bf16_t*>(&vg);
     const bf16_t* eu = reinterpret_cast<const bf16_t*>(&vu);
 #pragma unroll
@@ -191,8 +193,9 @@ at::Tensor swiglu_bwd(const at::Tensor& da, const at::Tensor& gu) {
   return dgu;
 }
 
-// (a [T, F], a^T [F, T]); T and F multiples of 64.
-std::tuple<at::Tensor, at::Tensor> swiglu_fwd_t(const at::Tensor& gu) {
+// (a [T, F], a^T [F, T]); T and F multiples of 64. plain=false: only a^T is written
+// (a is returned empty) for consumers that read the activation transposed.
+std::tuple<at::Tensor, at::Tensor> swiglu_fwd_t(const at::Tensor& gu, bool plain) {
   FT_CHECK_CUDA(gu);
   FT_CHECK_BF16(gu);
   FT_CHECK_CONTIG(gu);
@@ -200,17 +203,17 @@ std::tuple<at::Tensor, at::Tensor> swiglu_fwd_t(const at::Tensor& gu) {
   const int T = gu.numel() / (2 * F);
   TORCH_CHECK(F % TT == 0 && T % TT == 0, "swiglu_fwd_t: T and F must be multiples of 64");
   const at::DeviceGuard guard(gu.device());
-  auto a = at::empty({T, F}, gu.options());
+  auto a = plain ? at::empty({T, F}, gu.options()) : at::empty({0}, gu.options());
   auto aT = at::empty({F, T}, gu.options());
   if (T > 0)
     hipLaunchKernelGGL(swiglu_fwd_t_kernel, dim3((T / TT) * (F / TT)), dim3(256), 0, ft_stream(),
-                       cptr<bf16_t>(gu), mptr<bf16_t>(a), mptr<bf16_t>(aT), T, F);
+                       cptr<bf16_t>(gu), plain ? mptr<bf16_t>(a) : nullptr, mptr<bf16_t>(aT), T, F);
   FT_LAUNCH_CHECK();
   return {a, aT};
 }
 
-// (dgu [T, 2F], dgu^T [2F, T]); T and F multiples of 64.
-std::tuple<at::Tensor, at::Tensor> swiglu_bwd_t(const at::Tensor& da, const at::Tensor& gu) {
+// (dgu [T, 2F], dgu^T [2F, T]); T and F multiples of 64. plain=false: only dgu^T.
+std::tuple<at::Tensor, at::Tensor> swiglu_bwd_t(const at::Tensor& da, const at::Tensor& gu, bool plain) {
   FT_CHECK_CUDA(gu);
   FT_CHECK_BF16(gu);
   FT_CHECK_CONTIG(gu);
@@ -220,18 +223,19 @@ std::tuple<at::Tensor, at::Tensor> swiglu_bwd_t(const at::Tensor& da, const at::
   TORCH_CHECK(da.numel() == (long)T * F, "swiglu_bwd_t: shape mismatch");
   TORCH_CHECK(F % TT == 0 && T % TT == 0, "swiglu_bwd_t: T and F must be multiples of 64");
   const at::DeviceGuard guard(gu.device());
-  auto dgu = at::empty({T, 2 * F}, gu.options());
+  auto dgu = plain ? at::empty({T, 2 * F}, gu.options()) : at::empty({0}, gu.options());
   auto dguT = at::empty({2 * F, T}, gu.options());
   if (T > 0)
     hipLaunchKernelGGL(swiglu_bwd_t_kernel, dim3((T / TT) * (F / TT)), dim3(256), 0, ft_stream(),
-                       cptr<bf16_t>(da), cptr<bf16_t>(gu), mptr<bf16_t>(dgu), mptr<bf16_t>(dguT), T, F);
+                       cptr<bf16_t>(da), cptr<bf16_t>(gu), plain ? mptr<bf16_t>(dgu) : nullptr,
+                       mptr<bf16_t>(dguT), T, F);
   FT_LAUNCH_CHECK();
   return {dgu, dguT};
 }
 
 TORCH_LIBRARY_FRAGMENT(ftamd, m) {
-  m.def("swiglu_fwd_t(Tensor gu) -> (Tensor, Tensor)", &swiglu_fwd_t);
-  m.def("swiglu_bwd_t(Tensor da, Tensor gu) -> (Tensor, Tensor)", &swiglu_bwd_t);
+  m.def("swiglu_fwd_t(Tensor gu, bool plain=True) -> (Tensor, Tensor)", &swiglu_fwd_t);
+  m.def("swiglu_bwd_t(Tensor da, Tensor gu, bool plain=True) -> (Tensor, Tensor)", &swiglu_bwd_t);
   m.def("swiglu_fwd(Tensor gu) -> Tensor", &swiglu_fwd);
   m.def("swiglu_bwd(Tensor da, Tensor gu) -> Tensor", &swiglu_bwd);
 }

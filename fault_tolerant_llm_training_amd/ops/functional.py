@@ -69,14 +69,15 @@ def weight_grad(dy2: torch.Tensor, x2: torch.Tensor, sink: Optional[GradSink],
     return torch.mm(dy2.t(), x2)
 
 
-# Weight-gradient GEMMs on a side stream (FT_DW_STREAM=1): dW and the dX GEMM of the same
-# node are independent, and the small projections (wo, wqkv: 128-192 output tiles of
-# 256x256) leave half of the 256 CUs idle when run one after the other. The side stream
+# Weight-gradient GEMMs on a side stream (default; FT_DW_STREAM=0 disables): dW and the dX
+# GEMM of the same node are independent, and the small projections (wo, wqkv: 128-192
+# output tiles of 256x256) leave half of the 256 CUs idle when run one after the other
+# (8B step: 108.6 -> 107.1 ms, profiles/r1_dw_stream_ab.log). The side stream
 # waits for the compute stream before each dW (so it sees dY / X), the operands are
 # recorded on it (the caching allocator keeps them alive), and the bucket hooks fired
 # from it order the reducer's collectives after it. join_dw_stream() (GradReducer.finish,
 # FlatAdamW.step) makes the compute stream wait for every dW before the optimizer.
-_DW_STREAM = os.environ.get("FT_DW_STREAM", "0") == "1"
+_DW_STREAM = os.environ.get("FT_DW_STREAM", "1") == "1"
 _dw_streams = {}
 
 
@@ -403,6 +404,15 @@ def swiglu(gu):
 
 
 _FUSED_FFN = os.environ.get("FT_FUSED_FFN", "1") != "0"
+# FT_FFN_T_ONLY=1: the SwiGLU kernels write only the transposed activation / gradient and
+# the w2 forward and w13 dX GEMMs read those transposed (A^T operand), saving one
+# [T, F] and one [T, 2F] bf16 write per layer.
+_FFN_T_ONLY = os.environ.get("FT_FFN_T_ONLY", "0") == "1"
+
+
+def set_ffn_t_only(on: bool) -> None:
+    global _FFN_T_ONLY
+    _FFN_T_ONLY = bool(on)
 
 
 class FeedForwardFn(torch.autograd.Function):
@@ -420,13 +430,15 @@ class FeedForwardFn(torch.autograd.Function):
         x2 = x.reshape(-1, D)
         gu = torch.mm(x2, w13.t())
         tn = _use_tn(gu, x2)
+        t_only = tn and _FFN_T_ONLY
         if tn:
-            a, aT = K_.swiglu_fwd_t(gu)
+            a, aT = K_.swiglu_fwd_t(gu, not t_only)
         else:
             a, aT = K_.swiglu_fwd(gu), None
-        y = torch.mm(a, w2.t())
+        y = torch.mm(aT.t() if t_only else a, w2.t())
         ctx.sinks = (sink13, sink2)
         ctx.tn = tn
+        ctx.t_only = t_only
         ctx.xshape = x.shape
         ctx.save_for_backward(x2, gu, aT if tn else a, w13, w2)
         return y.view(*x.shape[:-1], w2.shape[0])
@@ -443,7 +455,9 @@ class FeedForwardFn(torch.autograd.Function):
             dw2 = weight_grad_async(dy2, a_or_T, sink2)
         da = torch.mm(dy2, w2)
         if ctx.tn:
-            dgu, dguT = K_.swiglu_bwd_t(da, gu)
+            dgu, dguT = K_.swiglu_bwd_t(da, gu, not ctx.t_only)
+            if ctx.t_only:
+                dgu = dguT.t()
         else:
             dgu, dguT = K_.swiglu_bwd(da, gu), None
         del da

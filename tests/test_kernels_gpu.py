@@ -197,6 +197,42 @@ def test_pipelined_optimizer_matches_serial(max_norm):
         assert rel(p0, p1) < 1e-2 and rel(s0[:1], s1[:1]) < 1e-2
 
 
+@pytest.mark.parametrize("dw_mode", ["all", "none"])
+def test_dw_side_stream_bitwise(dw_mode, monkeypatch):
+    """Weight-gradient GEMMs on the side stream (concurrent with dX) give bit-identical training."""
+    from fault_tolerant_llm_training_amd.models.llama import build_model, model_args_for
+    from fault_tolerant_llm_training_amd.ops import functional as Fx
+    from fault_tolerant_llm_training_amd.optim.adamw import FlatAdamW
+    from fault_tolerant_llm_training_amd.parallel.ddp import GradReducer
+
+    monkeypatch.setattr(Fx, "_DW_MODE", dw_mode)
+    a = model_args_for("tiny", vocab_size=1024, seq_len=256)
+    tok = torch.randint(0, 1024, (2, 256), device="cuda")
+    lab = torch.randint(0, 1024, (2, 256), device="cuda")
+    out = []
+    try:
+        for side in (False, True):
+            Fx.set_dw_stream(side)
+            m = build_model(a, "cuda", torch.bfloat16, seed=5)
+            red = GradReducer(m.flat, m.sinks_in_backward_order(), bucket_mb=0.25)
+            opt = FlatAdamW(m.parameters(), m.flat, lr=1e-2, max_grad_norm=1.0, reducer=red)
+            m.gate = opt.gate
+            losses = []
+            for _ in range(3):
+                loss = m(tok, lab)
+                loss.backward()
+                red.finish()
+                opt.step()
+                losses.append(loss.float())
+            opt.gate.wait_all()
+            torch.cuda.synchronize()
+            out.append((m.flat.params.clone(), m.flat.grads.clone(), torch.stack(losses)))
+    finally:
+        Fx.set_dw_stream(True)
+    (p0, g0, l0), (p1, g1, l1) = out
+    assert torch.equal(g0, g1) and torch.equal(p0, p1) and torch.equal(l0, l1)
+
+
 @pytest.mark.parametrize("R,C", [(64, 64), (2048, 4096), (128, 28672), (4096, 192)])
 def test_transpose2d(K, R, C):
     x = torch.randn(R, C, device="cuda").bfloat16()
@@ -263,14 +299,15 @@ def test_swiglu_transposed_outputs(K, T, F_):
     assert torch.equal(dgu, K.swiglu_bwd(da, gu)) and torch.equal(dguT, dgu.t().contiguous())
 
 
-@pytest.mark.parametrize("mode", ["all", "none"])
-def test_feed_forward_fused(mode, monkeypatch):
+@pytest.mark.parametrize("mode,t_only", [("all", False), ("all", True), ("none", False)])
+def test_feed_forward_fused(mode, t_only, monkeypatch):
     """FeedForwardFn (GEMM → tiled SwiGLU with transposed outputs → GEMM, weight grads into
     sinks) vs fp32 autograd of w2(silu(x w1^T) * (x w3^T))."""
     from fault_tolerant_llm_training_amd.ops import functional as Fx
     from fault_tolerant_llm_training_amd.ops.grad_sink import GradSink
 
     monkeypatch.setattr(Fx, "_DW_MODE", mode)
+    monkeypatch.setattr(Fx, "_FFN_T_ONLY", t_only)
     torch.manual_seed(5)
     T, D, Fh = 256, 192, 320
     x = torch.randn(T, D, device="cuda").bfloat16().requires_grad_(True)
