@@ -4,6 +4,7 @@
 Knobs toggled between timing windows (alternating rounds, so box and clock drift cancel):
   gemm  — TunableOp GEMM solution table (tuning/gemm_gfx950.csv) vs the hipBLASLt heuristic
   dw    — weight-gradient GEMMs on a side stream, concurrent with the dX GEMMs
+  dqs   — deterministic flash backward: dQ kernel on a second stream, concurrent with dK/dV
   tonly — SwiGLU kernels write only the transposed activation/gradient; the w2 forward and
           w13 dX GEMMs read them as A^T
 Usage: python scripts/ab_step.py [--steps 8] [--rounds 3] [--configs gemm,dw ...]
@@ -76,7 +77,10 @@ def main():
         return (time.perf_counter() - t) / n * 1e3
 
     knobs = [k for k in a.knobs.split(",") if k]
-    setters = {"gemm": gemm_tuning.set_enabled, "dw": Fx.set_dw_stream, "tonly": Fx.set_ffn_t_only}
+    from fault_tolerant_llm_training_amd._native import kernels
+
+    setters = {"gemm": gemm_tuning.set_enabled, "dw": Fx.set_dw_stream, "tonly": Fx.set_ffn_t_only,
+               "dqs": kernels().flash_set_dq_stream}
     configs = list(itertools.product([False, True], repeat=len(knobs)))
 
     def apply(cfg):
