@@ -4,6 +4,7 @@
 Knobs toggled between timing windows (alternating rounds, so box and clock drift cancel):
   gemm  — TunableOp GEMM solution table (tuning/gemm_gfx950.csv) vs the hipBLASLt heuristic
   dw    — weight-gradient GEMMs on a side stream, concurrent with the dX GEMMs
+  prio  — compute on a high-priority stream (its workgroups dispatch ahead of the side streams')
   dqs   — deterministic flash backward: dQ kernel on a second stream, concurrent with dK/dV
   tonly — SwiGLU kernels write only the transposed activation/gradient; the w2 forward and
           w13 dX GEMMs read them as A^T
@@ -79,8 +80,15 @@ def main():
     knobs = [k for k in a.knobs.split(",") if k]
     from fault_tolerant_llm_training_amd._native import kernels
 
+    hp = torch.cuda.Stream(device=dev, priority=-1)
+    default_stream = torch.cuda.current_stream(dev)
+
+    def set_prio(on):
+        torch.cuda.synchronize()
+        torch.cuda.set_stream(hp if on else default_stream)
+
     setters = {"gemm": gemm_tuning.set_enabled, "dw": Fx.set_dw_stream, "tonly": Fx.set_ffn_t_only,
-               "dqs": kernels().flash_set_dq_stream}
+               "dqs": kernels().flash_set_dq_stream, "prio": set_prio}
     configs = list(itertools.product([False, True], repeat=len(knobs)))
 
     def apply(cfg):
