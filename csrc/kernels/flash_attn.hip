@@ -55,30 +55,28 @@ __device__ __forceinline__ void static_for(F&& f) {
 
 constexpr float LOG2E_F = 1.4426950408889634f;
 
-// Byte offset of 16-B chunk c of row r in a [rows][D] bf16 LDS image.
+// Byte offset of 16-B chunk c of row r in a [rows][D] bf16 LDS image: 8-row x 32-column
+// (512-B) subtiles, 64-B subtile rows, the chunk's low two bits XORed with row bits 2-3
+// (cdna_hip_programming.md T10, image (a)). Conflict-free for the ds_read_b128 row reads
+// (16 lanes = 16 rows of one chunk) and for the 4-row ds_read_b64_tr_b16 transposed reads;
+// and since the XOR never touches the subtile index, reads of other 32-column blocks or
+// 8-row blocks are the same lane address plus an immediate, so the 16 transposed reads of
+// a 32x32x16 operand sweep share two address registers (the compiler can then keep reads
+// in flight ahead of the MFMAs instead of rematerialising addresses).
 template <int D>
 __device__ __forceinline__ int lds_off(int r, int c) {
-  if constexpr (D == 128) {
-    return r * 256 + 16 * (c ^ (((r & 3) << 2) | ((r >> 2) & 3)));
-  } else {
-    static_assert(D == 64, "head_dim must be 64 or 128");
-    const int R = r >> 1, C = 8 * (r & 1) + c;
-    return R * 256 + 16 * (C ^ (((R & 3) << 2) | ((R >> 2) & 3)));
-  }
+  static_assert(D == 64 || D == 128, "head_dim must be 64 or 128");
+  return (r >> 3) * (16 * D) + 512 * (c >> 2) + 64 * (r & 7) + 16 * ((c & 3) ^ ((r >> 2) & 3));
 }
 
 // Inverse of lds_off: which (row, chunk) lives at 16-B slot P of the image.
 template <int D>
 __device__ __forceinline__ void lds_inv(int P, int& r, int& c) {
-  const int R = P >> 4, Cp = P & 15;
-  const int C = Cp ^ (((R & 3) << 2) | ((R >> 2) & 3));
-  if constexpr (D == 128) {
-    r = R;
-    c = C;
-  } else {
-    r = 2 * R + (C >> 3);
-    c = C & 7;
-  }
+  const int byte = P * 16;
+  const int rb = byte / (16 * D), rem = byte % (16 * D);
+  const int sub = rem >> 9, r7 = (rem >> 6) & 7, x = (rem >> 4) & 3;
+  r = rb * 8 + r7;
+  c = sub * 4 + (x ^ ((r >> 2) & 3));
 }
 
 // LDS-DMA (global_load_lds_dwordx4): each lane moves 16 B to lds_base + lane * 16.

@@ -8,13 +8,16 @@ backend used by the gloo/CPU tests, not a GPU fallback).
 from __future__ import annotations
 
 import importlib.util
+import os
 import threading
 from pathlib import Path
 
 import torch
 
 _PKG = Path(__file__).resolve().parent
-KERNELS_SO = _PKG / "_kernels.so"
+# FT_KERNELS_SO: load another build of the kernel library (A/B of two kernel builds in
+# separate processes, scripts/flash_bench.py); unset = the in-tree build
+KERNELS_SO = Path(os.environ.get("FT_KERNELS_SO") or (_PKG / "_kernels.so"))
 RUNTIME_SO = _PKG / "_runtime.so"
 
 _lock = threading.Lock()
