@@ -54,6 +54,7 @@ __device__ __forceinline__ void static_for(F&& f) {
 }
 
 constexpr float LOG2E_F = 1.4426950408889634f;
+constexpr float RESCALE_LOG2 = 8.f;  // forward: deferred-rescale threshold (log2 units)
 
 // Byte offset of 16-B chunk c of row r in a [rows][D] bf16 LDS image: 8-row x 32-column
 // (512-B) subtiles, 64-B subtile rows, the chunk's low two bits XORed with row bits 2-3
@@ -141,6 +142,14 @@ __device__ __forceinline__ f32x16_t mfma32(bf16x8_t a, bf16x8_t b, f32x16_t c) {
 // Raw v_exp_f32 (2^x): exp2f adds denormal range-reduction (cmp + cndmask + ldexp per
 // call) that softmax does not need — its arguments are <= 0 and tiny results flush to 0.
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// max(x[lane], x[lane ^ 32]) with one v_permlane32_swap (no LDS round trip, unlike the
+// ds_bpermute behind __shfl_xor): swapping x with itself leaves the low half of the wave
+// in one result and the high half in the other, on every lane.
+__device__ __forceinline__ float max_lane32(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
 
 // lse2 / delta rows are padded to a multiple of 32 queries, so a 32-query slice's
 // statistics are whole, aligned float4s (padding entries are never used unmasked).
@@ -278,26 +287,35 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(const bf16_t* __restr
           }
           mx = fmaxf(mx, x);
         }
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float mn = fmaxf(m, mx * sl2);
-      const float alpha = fast_exp2(m - mn);
-      m = mn;
+      mx = max_lane32(mx);
+      // Deferred rescale (cdna_hip_programming.md T13): the running max only moves when
+      // some row of the wave grew by more than RESCALE_LOG2 (in log2 units); otherwise P
+      // is exponentiated against the stale max (values up to 2^RESCALE_LOG2, exact in the
+      // fp32 accumulators, same relative bf16 rounding) and the O / l rescale is skipped.
+      // The decision precedes this tile's exponentials, so nothing is ever half-scaled.
+      const float cand = mx * sl2;
+      if (__any(cand > m + RESCALE_LOG2)) {
+        const float mn = fmaxf(m, cand);
+        const float alpha = fast_exp2(m - mn);
+        m = mn;
+        l *= alpha;
+#pragma unroll
+        for (int db = 0; db < NDB; ++db)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) o[db][r] *= alpha;
+      }
       float ls = 0.f;
 #pragma unroll
       for (int j = 0; j < 2; ++j)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const float p = fast_exp2(fmaf(s[j][r], sl2, -mn));
+          const float p = fast_exp2(fmaf(s[j][r], sl2, -m));
           ls += p;
           s[j][r] = p;
         }
       const bf16x8_t pb00 = cvt8<0>(s[0]), pb01 = cvt8<8>(s[0]);
       const bf16x8_t pb10 = cvt8<0>(s[1]), pb11 = cvt8<8>(s[1]);
-      l = l * alpha + ls;
-#pragma unroll
-      for (int db = 0; db < NDB; ++db)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) o[db][r] *= alpha;
+      l += ls;
 #pragma unroll
       for (int db = 0; db < NDB; ++db) {
         o[db] = mfma32(tr_frag<D>(vb, 0, db * 32, lane), pb00, o[db]);

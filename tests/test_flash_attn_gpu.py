@@ -76,3 +76,27 @@ def test_flash_bwd_deterministic_mode_is_bitwise_reproducible():
     assert torch.equal(a, b)
     c = K.flash_bwd(do, qk, qkv, o, lse, S, Hq, Hkv, D, 0)
     assert ((a.float() - c.float()).norm() / c.float().norm()).item() < 1e-2
+
+
+@pytest.mark.parametrize("slope", [0.02, 0.07, 0.3])
+def test_flash_fwd_growing_scores(slope):
+    """Scores that grow along the key axis at several rates, so the forward's running max moves
+    by amounts around the deferred-rescale threshold on many tiles (rare on random data)."""
+    from fault_tolerant_llm_training_amd._native import kernels
+
+    K = kernels()
+    torch.manual_seed(1)
+    S, Hq, Hkv, D = 1024, 4, 2, 128
+    q = torch.randn(S, Hq, D, device="cuda")
+    u = torch.nn.functional.normalize(torch.randn(D, device="cuda"), dim=0)
+    q = q + 4.0 * u  # every query has a component along u
+    ramp = slope * torch.arange(S, device="cuda", dtype=torch.float32).view(S, 1, 1)
+    k = 0.5 * torch.randn(S, Hkv, D, device="cuda") + ramp * u  # later keys score higher
+    v = torch.randn(S, Hkv, D, device="cuda")
+    qk = torch.cat([q.reshape(S, -1), k.reshape(S, -1)], 1).bfloat16()
+    qkv = torch.cat([qk, v.reshape(S, -1).bfloat16()], 1)
+    o, _ = K.flash_fwd(qk, qkv, S, Hq, Hkv, D)
+    ref = ref_attn(qk[:, : Hq * D].float().view(1, S, Hq, D), qk[:, Hq * D :].float().view(1, S, Hkv, D),
+                   v.bfloat16().float().view(1, S, Hkv, D))
+    assert torch.isfinite(o).all()
+    assert rel(o.view(1, S, Hq, D), ref) < 1e-2
