@@ -398,7 +398,7 @@ template <int D, int DQ = 0>
 __global__ __launch_bounds__(256, 1) void flash_bwd_kernel(
     const bf16_t* __restrict__ dO, const bf16_t* __restrict__ qk, const bf16_t* __restrict__ qkv,
     const float* __restrict__ lse2, const float* __restrict__ delta, float* __restrict__ dq_acc,
-    float* __restrict__ dk_part, float* __restrict__ dv_part, int B, int S, int Hq, int Hkv,
+    bf16_t* __restrict__ dk_part, bf16_t* __restrict__ dv_part, int B, int S, int Hq, int Hkv,
     float sl2, float scale) {
   constexpr int BK = 128, BQ = 32, KS = D / 16, NDB = D / 32, DCH = D / 8;
   constexpr int KIMG = BK * D * 2;   // K image (keys x D)
@@ -609,7 +609,9 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_kernel(
   }
 #undef BWD_GLDS
 
-  // dK / dV partials of this q-head (C layout: lane -> d, registers -> keys)
+  // dK / dV of this q-head, rounded to bf16 like the per-head gradients of the reference's
+  // repeat_kv + SDPA path; the finalize kernel sums the GQA group in fp32
+  // (C layout: lane -> d, registers -> keys)
 #pragma unroll
   for (int db = 0; db < NDB; ++db)
 #pragma unroll
@@ -617,8 +619,8 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_kernel(
       const int k = kw + (r & 3) + 8 * (r >> 2) + 4 * hi;
       if (k < S) {
         const long off = ((long)b * S + k) * ldo + (long)h * D + db * 32 + l32;
-        dk_part[off] = dk[db][r] * scale;
-        dv_part[off] = dv[db][r];
+        dk_part[off] = f2bf(dk[db][r] * scale);
+        dv_part[off] = f2bf(dv[db][r]);
       }
     }
 }
@@ -791,8 +793,8 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dq_kernel(
 
 // dqkv[:, q | k | v] = bf16(dQ), bf16(sum_G dK_part), bf16(sum_G dV_part)
 __global__ __launch_bounds__(256) void flash_bwd_finalize_kernel(
-    const float* __restrict__ dq_acc, const float* __restrict__ dk_part,
-    const float* __restrict__ dv_part, bf16_t* __restrict__ dqkv, long T, int Hq, int Hkv, int D) {
+    const float* __restrict__ dq_acc, const bf16_t* __restrict__ dk_part,
+    const bf16_t* __restrict__ dv_part, bf16_t* __restrict__ dqkv, long T, int Hq, int Hkv, int D) {
   const int G = Hq / Hkv;
   const int W = (Hq + 2 * Hkv) * D;
   const int vpr = W / 4;
@@ -808,11 +810,12 @@ __global__ __launch_bounds__(256) void flash_bwd_finalize_kernel(
       const bool isk = col < (Hq + Hkv) * D;
       const int c2 = col - (isk ? Hq * D : (Hq + Hkv) * D);
       const int kh = c2 / D, d = c2 % D;
-      const float* src = (isk ? dk_part : dv_part) + t * Hq * D + (long)kh * G * D + d;
+      const bf16_t* src = (isk ? dk_part : dv_part) + t * Hq * D + (long)kh * G * D + d;
       v = make_float4(0.f, 0.f, 0.f, 0.f);
       for (int r = 0; r < G; ++r) {
-        const float4 x = *reinterpret_cast<const float4*>(src + r * D);
-        v.x += x.x; v.y += x.y; v.z += x.z; v.w += x.w;
+        const uint2 x = *reinterpret_cast<const uint2*>(src + r * D);
+        v.x += __uint_as_float(x.x << 16); v.y += __uint_as_float(x.x & 0xffff0000u);
+        v.z += __uint_as_float(x.y << 16); v.w += __uint_as_float(x.y & 0xffff0000u);
       }
     }
     uint2 o;
@@ -914,8 +917,8 @@ at::Tensor flash_bwd(const at::Tensor& dout, const at::Tensor& qk, const at::Ten
   // mode 2: timing experiment only (racy dQ stores).
   const bool det = mode == 1;
   at::Tensor dq_acc = det ? at::Tensor() : (mode == 2 ? at::empty({T, Hq * D}, f32) : at::zeros({T, Hq * D}, f32));
-  auto dk_part = at::empty({T, Hq * D}, f32);
-  auto dv_part = at::empty({T, Hq * D}, f32);
+  auto dk_part = at::empty({T, Hq * D}, qk.options());
+  auto dv_part = at::empty({T, Hq * D}, qk.options());
   auto dqkv = at::empty({T, (Hq + 2 * Hkv) * D}, qk.options());
   const float sl2 = LOG2E_F / std::sqrt((float)D);
   const float scale = 1.f / std::sqrt((float)D);
@@ -927,7 +930,7 @@ at::Tensor flash_bwd(const at::Tensor& dout, const at::Tensor& qk, const at::Ten
 #define FT_BWD(DD, MODE)                                                                          \
   hipLaunchKernelGGL((flash_bwd_kernel<DD, MODE>), grid, block, 0, ft_stream(), cptr<bf16_t>(dout), \
                      cptr<bf16_t>(qk), cptr<bf16_t>(qkv), cptr<float>(lse), cptr<float>(delta),     \
-                     dqp, mptr<float>(dk_part), mptr<float>(dv_part), B, (int)S, (int)Hq, (int)Hkv, \
+                     dqp, mptr<bf16_t>(dk_part), mptr<bf16_t>(dv_part), B, (int)S, (int)Hq, (int)Hkv, \
                      sl2, scale)
   // dQ kernel stream: a side stream forked from (and joined back into) the caller's stream
   DqSide* side = det ? dq_side() : nullptr;
@@ -968,7 +971,7 @@ at::Tensor flash_bwd(const at::Tensor& dout, const at::Tensor& qk, const at::Ten
   const long vec = (long)T * ((Hq + 2 * Hkv) * D / 4);
   const int fin_blocks = (int)std::max(1L, std::min((vec + 255) / 256, 4096L));
   hipLaunchKernelGGL(flash_bwd_finalize_kernel, dim3(fin_blocks), block, 0, ft_stream(),
-                     det ? nullptr : cptr<float>(dq_acc), cptr<float>(dk_part), cptr<float>(dv_part),
+                     det ? nullptr : cptr<float>(dq_acc), cptr<bf16_t>(dk_part), cptr<bf16_t>(dv_part),
                      mptr<bf16_t>(dqkv), (long)T, (int)Hq, (int)Hkv, (int)D);
   FT_LAUNCH_CHECK();
   return dqkv;
