@@ -119,7 +119,8 @@ def main():
     _sync(dev)
     elapsed = time.perf_counter() - t0
     elapsed = fdist.ctrl_allreduce_max(int(elapsed * 1e9)) / 1e9
-    final_loss = float(loss.item())
+    # each rank's loss is its token sum over the GLOBAL token count: the global mean is the sum
+    final_loss = fdist.ctrl_allreduce_sum(float(loss.item())) if world > 1 else float(loss.item())
     opt.check_finite(block=True)
 
     ms = elapsed / a.steps * 1e3
