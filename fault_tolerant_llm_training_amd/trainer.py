@@ -347,6 +347,11 @@ def train(args) -> int:
                 extra = {"lr": f"{lr_now:.3e}"}
                 if device.type == "cuda":
                     extra["peak_HBM_GB"] = f"{torch.cuda.max_memory_allocated(device) / 2**30:.1f}"
+                if info.distributed:
+                    # each rank's loss is its token sum over the GLOBAL token count: the
+                    # logged global-batch mean is their sum (every rank logs at the same steps)
+                    loss = loss.detach().clone()
+                    torch.distributed.all_reduce(loss)
                 losslog.push(training_step, loss, extra, norm=optimizer.norm_for_logging())
                 if metrics_f is not None:
                     now = time.perf_counter()
