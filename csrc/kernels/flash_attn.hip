@@ -638,10 +638,15 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dq_kernel(
     const bf16_t* __restrict__ dO, const bf16_t* __restrict__ qk, const bf16_t* __restrict__ qkv,
     const float* __restrict__ lse2, const float* __restrict__ delta, bf16_t* __restrict__ dqkv, int B,
     int S, int Hq, int Hkv, float sl2, float scale) {
-  constexpr int BM = 128, BN = 64, KS = D / 16, NDB = D / 32, DCH = D / 8;
+  constexpr int BM = 128, BN = 64, KS = D / 16, NDB = D / 32;
   constexpr int TILE = BN * D * 2;
-  constexpr int CPT = BN * DCH / 256;
-  __shared__ __attribute__((aligned(16))) char smem[4 * TILE];
+  // K | V tiles arrive by LDS-DMA (no staging VGPRs held across the compute: at one wave
+  // per SIMD the register-staged prefetch pushed the dQ accumulators through AGPR copies
+  // every tile). Two separate LDS objects + a loop unrolled by two: every LDS read names
+  // a buffer the in-flight DMA provably does not write, so the compiler never drains the
+  // prefetch before reading the current tile.
+  __shared__ __attribute__((aligned(16))) char kv0[2 * TILE];
+  __shared__ __attribute__((aligned(16))) char kv1[2 * TILE];
 
   const int nqt = (S + BM - 1) / BM;
   const int per = B * Hq;
@@ -673,37 +678,29 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dq_kernel(
 
   const int kend = min((qt + 1) * BM, S);
   const int ntiles = (kend + BN - 1) / BN;
-  u32x4 kr[CPT], vr[CPT];
-  int srow[CPT], soff[CPT];
-  static_for<CPT>([&](auto I) {
-    const int id = tid + I * 256;
-    srow[I] = id / DCH;
-    soff[I] = lds_off<D>(id / DCH, id % DCH);
-  });
-  const bf16_t* Kc = Kg + (tid % DCH) * 8;
-  const bf16_t* Vc = Vg + (tid % DCH) * 8;
-#define DQ_GLOAD(KT)                                                         \
-  static_for<CPT>([&](auto I) {                                              \
-    const long key = min((KT) * BN + srow[I], S - 1);                        \
-    kr[I] = *reinterpret_cast<const u32x4*>(Kc + key * ldqk);                \
-    vr[I] = *reinterpret_cast<const u32x4*>(Vc + key * ldv);                 \
-  });
-#define DQ_SWRITE(BUF)                                                       \
-  static_for<CPT>([&](auto I) {                                              \
-    char* kb_ = smem + (BUF) * 2 * TILE;                                     \
-    *reinterpret_cast<u32x4*>(kb_ + soff[I]) = kr[I];                        \
-    *reinterpret_cast<u32x4*>(kb_ + TILE + soff[I]) = vr[I];                 \
-  });
+  constexpr int GPW = TILE / 1024 / 4;  // glds instructions per wave per image
+  // tile KT -> buffer BUF: each lane moves one 16-B chunk; the swizzle is on the source
+  auto dma = [&](int KT, auto BUF) {
+    char* kb_ = decltype(BUF)::value ? kv1 : kv0;
+    static_for<GPW>([&](auto I) {
+      const int piece = wave * GPW + I;
+      int r, c;
+      lds_inv<D>(piece * 64 + lane, r, c);
+      const long key = min(KT * BN + r, S - 1);
+      glds16(Kg + key * ldqk + c * 8, kb_ + piece * 1024);
+      glds16(Vg + key * ldv + c * 8, kb_ + TILE + piece * 1024);
+    });
+  };
 
-  DQ_GLOAD(0)
-  DQ_SWRITE(0)
-  __syncthreads();
+  dma(0, std::integral_constant<int, 0>{});
   // Materialise the Q / dO fragments and row statistics before the loop: left pending,
   // the compiler's waits for them inside the loop would drain the next tile's prefetch.
   asm volatile("" ::"v"(lq), "v"(dlq));
   static_for<KS>([&qf, &df](auto I) {
     asm volatile("" ::"v"(__builtin_bit_cast(u32x4, qf[I])), "v"(__builtin_bit_cast(u32x4, df[I])));
   });
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
 
   f32x16_t dq[NDB];
 #pragma unroll
@@ -711,12 +708,10 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dq_kernel(
 #pragma unroll
     for (int r = 0; r < 16; ++r) dq[db][r] = 0.f;
 
-  for (int kt = 0; kt < ntiles; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < ntiles) {
-      DQ_GLOAD(kt + 1)
-    }
-    const char* kb = smem + cur * 2 * TILE;
+  auto iter = [&](const int kt, auto CUR) {
+    constexpr int cur = decltype(CUR)::value;
+    if (kt + 1 < ntiles) dma(kt + 1, std::integral_constant<int, cur ^ 1>{});
+    const char* kb = cur ? kv1 : kv0;
     const char* vb = kb + TILE;
     const int k0 = kt * BN;
     const bool v0 = k0 <= q0 + 31;
@@ -769,13 +764,13 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dq_kernel(
       else
         tile(std::false_type{});
     }
-    if (kt + 1 < ntiles) {
-      DQ_SWRITE(cur ^ 1)
-    }
-    __syncthreads();
+    __builtin_amdgcn_s_waitcnt(0);  // this wave's DMA of tile kt+1 has landed ...
+    __syncthreads();                // ... and everyone's; nobody reads tile kt any more
+  };
+  for (int kt = 0; kt < ntiles; kt += 2) {
+    iter(kt, std::integral_constant<int, 0>{});
+    if (kt + 1 < ntiles) iter(kt + 1, std::integral_constant<int, 1>{});
   }
-#undef DQ_GLOAD
-#undef DQ_SWRITE
 
   if (qrow < S) {
     bf16_t* orow = dqkv + ((long)b * S + qrow) * ldv + (long)h * D;
