@@ -170,10 +170,12 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(const bf16_t* __restr
                                                            bf16_t* __restrict__ out,
                                                            float* __restrict__ lse2, int B, int S,
                                                            int Hq, int Hkv, float sl2) {
-  constexpr int BM = 128, BN = 64, KS = D / 16, NDB = D / 32, DCH = D / 8;
+  constexpr int BM = 128, BN = 64, KS = D / 16, NDB = D / 32;
   constexpr int TILE = BN * D * 2;
-  constexpr int CPT = BN * DCH / 256;
-  __shared__ __attribute__((aligned(16))) char smem[4 * TILE];
+  // K | V tiles by LDS-DMA into two separate LDS objects, loop unrolled by two (as in the
+  // dQ kernel): no staging VGPRs live across the tile's compute, no drained prefetch.
+  __shared__ __attribute__((aligned(16))) char kv0[2 * TILE];
+  __shared__ __attribute__((aligned(16))) char kv1[2 * TILE];
 
   const int nqt = (S + BM - 1) / BM;
   const int per = B * Hq;
@@ -210,33 +212,19 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(const bf16_t* __restr
 
   const int kend = min((qt + 1) * BM, S);
   const int ntiles = (kend + BN - 1) / BN;
-  u32x4 kr[CPT], vr[CPT];
-  // loop-invariant per-thread staging coordinates (row within the tile, 16-B chunk)
-  int srow[CPT], soff[CPT];
-  static_for<CPT>([&](auto I) {
-    const int id = tid + I * 256;
-    srow[I] = id / DCH;
-    soff[I] = lds_off<D>(id / DCH, id % DCH);
-  });
-  static_assert(256 % DCH == 0, "staging chunk must be the same for every I");
-  const bf16_t* Kc = Kg + (tid % DCH) * 8;  // 256 is a multiple of DCH: same chunk for all I
-  const bf16_t* Vc = Vg + (tid % DCH) * 8;
-#define FWD_GLOAD(KT)                                                        \
-  static_for<CPT>([&](auto I) {                                              \
-    const long key = min((KT) * BN + srow[I], S - 1);                        \
-    kr[I] = *reinterpret_cast<const u32x4*>(Kc + key * ldqk);                \
-    vr[I] = *reinterpret_cast<const u32x4*>(Vc + key * ldv);                 \
-  });
-#define FWD_SWRITE(BUF)                                                      \
-  static_for<CPT>([&](auto I) {                                              \
-    char* kb_ = smem + (BUF) * 2 * TILE;                                     \
-    *reinterpret_cast<u32x4*>(kb_ + soff[I]) = kr[I];                        \
-    *reinterpret_cast<u32x4*>(kb_ + TILE + soff[I]) = vr[I];                 \
-  });
-
-  FWD_GLOAD(0)
-  FWD_SWRITE(0)
-  __syncthreads();
+  constexpr int GPW = TILE / 1024 / 4;  // glds instructions per wave per image
+  auto dma = [&](int KT, auto BUF) {
+    char* kb_ = decltype(BUF)::value ? kv1 : kv0;
+    static_for<GPW>([&](auto I) {
+      const int piece = wave * GPW + I;
+      int r, c;
+      lds_inv<D>(piece * 64 + lane, r, c);
+      const long key = min(KT * BN + r, S - 1);
+      glds16(Kg + key * ldqk + c * 8, kb_ + piece * 1024);
+      glds16(Vg + key * ldv + c * 8, kb_ + TILE + piece * 1024);
+    });
+  };
+  dma(0, std::integral_constant<int, 0>{});
 
   f32x16_t o[NDB];
 #pragma unroll
@@ -247,13 +235,13 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(const bf16_t* __restr
   // Materialise the Q fragments before the loop: left pending, the compiler's waits for
   // them inside the loop would also drain the next tile's prefetch (in-order vmcnt).
   static_for<KS>([&qf](auto I) { asm volatile("" ::"v"(__builtin_bit_cast(u32x4, qf[I]))); });
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
 
-  for (int kt = 0; kt < ntiles; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < ntiles) {
-      FWD_GLOAD(kt + 1)
-    }
-    const char* kb = smem + cur * 2 * TILE;
+  auto iter = [&](const int kt, auto CUR) {
+    constexpr int cur = decltype(CUR)::value;
+    if (kt + 1 < ntiles) dma(kt + 1, std::integral_constant<int, cur ^ 1>{});
+    const char* kb = cur ? kv1 : kv0;
     const char* vb = kb + TILE;
     const int k0 = kt * BN;
     const bool v0 = k0 <= q0 + 31;       // wave-uniform: sub-tile 0 has an unmasked key
@@ -335,13 +323,13 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(const bf16_t* __restr
       else
         tile(std::false_type{});
     }
-    if (kt + 1 < ntiles) {
-      FWD_SWRITE(cur ^ 1)
-    }
-    __syncthreads();
+    __builtin_amdgcn_s_waitcnt(0);  // this wave's DMA of tile kt+1 has landed ...
+    __syncthreads();                // ... and everyone's; nobody reads tile kt any more
+  };
+  for (int kt = 0; kt < ntiles; kt += 2) {
+    iter(kt, std::integral_constant<int, 0>{});
+    if (kt + 1 < ntiles) iter(kt + 1, std::integral_constant<int, 1>{});
   }
-#undef FWD_GLOAD
-#undef FWD_SWRITE
 
   l += __shfl_xor(l, 32, 64);
   const float inv = 1.f / l;
