@@ -613,6 +613,199 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_kernel(
     }
 }
 
+// ================================================================== backward dK/dV, slice pairs (deterministic)
+// flash_bwd_kernel<D, 1> with TWO independent 32-query slices per loop iteration: S / dP
+// of both slices are issued back to back, and in the steady state (both slices fully
+// below the diagonal) the whole pair is one basic block, so the scheduler can run slice
+// A's softmax VALU and dV / dK MFMAs while slice B's S / dP MFMAs are in flight (at one
+// wave per SIMD there is no other wave to fill the MFMA pipe during a softmax phase).
+// Q | dO pairs by LDS-DMA, double-buffered in two LDS objects (loop unrolled by two);
+// the slices' lse / delta ride along in LDS (registers are the scarce resource here).
+template <int D>
+__global__ __launch_bounds__(256, 1) void flash_bwd_dkdv2_kernel(
+    const bf16_t* __restrict__ dO, const bf16_t* __restrict__ qk, const bf16_t* __restrict__ qkv,
+    const float* __restrict__ lse2, const float* __restrict__ delta, bf16_t* __restrict__ dk_part,
+    bf16_t* __restrict__ dv_part, int B, int S, int Hq, int Hkv, float sl2, float scale) {
+  constexpr int BK = 128, BQ = 32, KS = D / 16, NDB = D / 32;
+  constexpr int QIMG = BQ * D * 2;          // one Q or dO slice
+  constexpr int SLOT = 2 * QIMG + 256;      // Q | dO | lse[32] | delta[32] of one slice
+  __shared__ __attribute__((aligned(16))) char pb0[2 * SLOT];  // pair buffer 0: slice A | slice B
+  __shared__ __attribute__((aligned(16))) char pb1[2 * SLOT];  // pair buffer 1
+
+  const int per = B * Hq;
+  const int L = blockIdx.x;
+  const int kt = L / per;  // key tile; kt = 0 has the most query slices -> launched first
+  const int rem = L % per;
+  const int b = rem / Hq;
+  int h, kvh;
+  map_head(rem % Hq, Hq, Hkv, h, kvh);
+
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, l32 = lane & 31, hi = lane >> 5;
+  const int kb0 = kt * BK;
+  const int kw = kb0 + wave * 32;  // this wave's first key
+  const long ldqk = (long)(Hq + Hkv) * D, ldv = (long)(Hq + 2 * Hkv) * D, ldo = (long)Hq * D;
+  const bf16_t* Qg = qk + (long)b * S * ldqk + (long)h * D;
+  const bf16_t* Kg = qk + (long)b * S * ldqk + (long)(Hq + kvh) * D;
+  const bf16_t* Vg = qkv + (long)b * S * ldv + (long)(Hq + Hkv + kvh) * D;
+  const bf16_t* dOg = dO + (long)b * S * ldo + (long)h * D;
+  const float* lseg = lse2 + ((long)b * Hq + h) * stat_stride(S);
+  const float* delg = delta + ((long)b * Hq + h) * stat_stride(S);
+
+  bf16x8_t vf[KS], kf[KS];
+  {
+    const long key = min(kw + l32, S - 1);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      vf[ks] = *reinterpret_cast<const bf16x8_t*>(Vg + key * ldv + ks * 16 + hi * 8);
+      kf[ks] = *reinterpret_cast<const bf16x8_t*>(Kg + key * ldqk + ks * 16 + hi * 8);
+    }
+  }
+
+  const int qs0 = kb0 / BQ;
+  const int n = (S + BQ - 1) / BQ - qs0;  // slices of this key tile (>= 1)
+  const int npairs = (n + 1) / 2;
+  constexpr int GPW = QIMG / 1024 / 4;    // glds instructions per wave per image
+  // pair p -> buffer: slices 2p (A) and 2p+1 (B, if any)
+  auto dma = [&](int p, char* buf) __attribute__((always_inline)) {
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      const int i = 2 * p + half;
+      if (i < n) {  // block-uniform
+        char* sl = buf + half * SLOT;
+        const int q0 = (qs0 + i) * BQ;
+        static_for<GPW>([&](auto I) {
+          const int piece = wave * GPW + I;
+          int r, c;
+          lds_inv<D>(piece * 64 + lane, r, c);
+          const long q = min(q0 + r, S - 1);
+          glds16(Qg + q * ldqk + c * 8, sl + piece * 1024);
+          glds16(dOg + q * ldo + c * 8, sl + QIMG + piece * 1024);
+        });
+        if (wave == half && lane < 16) {
+          // lanes 0-7: lse rows q0..q0+31, lanes 8-15: delta (rows padded to 32: in bounds)
+          const float* src = lane < 8 ? lseg + q0 + 4 * lane : delg + q0 + 4 * (lane - 8);
+          glds16(src, sl + 2 * QIMG);
+        }
+      }
+    }
+  };
+
+  f32x16_t dk[NDB], dv[NDB];
+#pragma unroll
+  for (int db = 0; db < NDB; ++db)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dk[db][r] = dv[db][r] = 0.f;
+
+  const int key = kw + l32;
+  auto sdp = [&](const char* sl, f32x16_t& sv, f32x16_t& dpv) __attribute__((always_inline)) {
+    const char* qi = sl;
+    const char* di = sl + QIMG;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) sv[r] = dpv[r] = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      sv = mfma32(ld_row<D>(qi, l32, 2 * ks + hi), kf[ks], sv);
+      dpv = mfma32(ld_row<D>(di, l32, 2 * ks + hi), vf[ks], dpv);
+    }
+  };
+  auto fin = [&](const char* sl, const int i, f32x16_t sv, f32x16_t dpv, auto MASKED)
+      __attribute__((always_inline)) {
+    constexpr bool MASK = decltype(MASKED)::value;
+    const char* qi = sl;
+    const char* di = sl + QIMG;
+    const float* st = reinterpret_cast<const float*>(sl + 2 * QIMG);
+    const int qb = (qs0 + i) * BQ;
+    static_for<4>([&](auto G) {
+      constexpr int g = G;
+      const float4 l4 = *reinterpret_cast<const float4*>(st + 8 * g + 4 * hi);
+      const float4 d4 = *reinterpret_cast<const float4*>(st + BQ + 8 * g + 4 * hi);
+      const float lv[4] = {l4.x, l4.y, l4.z, l4.w};
+      const float dv4[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int r = 4 * g + t;
+        float p = fast_exp2(fmaf(sv[r], sl2, -lv[t]));
+        float ds = p * (dpv[r] - dv4[t]);
+        if constexpr (MASK) {
+          // also covers padded rows q >= S, whose lse / delta are uninitialised
+          const int q = qb + 8 * g + 4 * hi + t;
+          const bool off = key > q || q >= S;
+          p = off ? 0.f : p;
+          ds = off ? 0.f : ds;
+        }
+        dpv[r] = ds;
+        sv[r] = p;
+      }
+    });
+    const bf16x8_t pa[2] = {cvt8<0>(sv), cvt8<8>(sv)};
+    const bf16x8_t da[2] = {cvt8<0>(dpv), cvt8<8>(dpv)};
+#pragma unroll
+    for (int ss = 0; ss < 2; ++ss)
+#pragma unroll
+      for (int db = 0; db < NDB; ++db) {
+        dv[db] = mfma32(pa[ss], tr_frag<D>(di, 16 * ss, db * 32, lane), dv[db]);
+        dk[db] = mfma32(da[ss], tr_frag<D>(qi, 16 * ss, db * 32, lane), dk[db]);
+      }
+  };
+  // one slice, general case (inactive / masked / ragged)
+  auto one = [&](const char* sl, const int i) __attribute__((always_inline)) {
+    const int qb = (qs0 + i) * BQ;
+    if (qb + BQ - 1 < kw) return;  // wave-uniform: all of the slice is above this wave's keys
+    f32x16_t sv, dpv;
+    sdp(sl, sv, dpv);
+    if (kw + 31 > qb || qb + BQ > S)
+      fin(sl, i, sv, dpv, std::true_type{});
+    else
+      fin(sl, i, sv, dpv, std::false_type{});
+  };
+
+  dma(0, pb0);
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  auto iter = [&](const int p, auto BUF) __attribute__((always_inline)) {
+    constexpr int bb = decltype(BUF)::value;
+    char* cur = bb ? pb1 : pb0;
+    if (p + 1 < npairs) dma(p + 1, bb ? pb0 : pb1);
+    const int ia = 2 * p, ib = 2 * p + 1;
+    const int qa = (qs0 + ia) * BQ;
+    // steady state: both slices entirely below this wave's diagonal and inside S
+    if (ib < n && qa >= kw + 31 && qa + 2 * BQ <= S) {
+      f32x16_t sa, dpa, sb, dpb;
+      // the compiler's default schedule keeps the pair's phases apart; the IGLP
+      // "DS + MFMA interleave" strategy spreads the LDS reads and the VALU between the
+      // MFMAs (measured: 193.8 -> 182.4 us for the whole deterministic backward; iglp_opt(1)
+      // 198.7 us)
+      __builtin_amdgcn_iglp_opt(0);
+      sdp(cur, sa, dpa);
+      sdp(cur + SLOT, sb, dpb);
+      fin(cur, ia, sa, dpa, std::false_type{});
+      fin(cur + SLOT, ib, sb, dpb, std::false_type{});
+    } else {
+      one(cur, ia);
+      if (ib < n) one(cur + SLOT, ib);
+    }
+    __builtin_amdgcn_s_waitcnt(0);  // this wave's DMA of pair p+1 has landed ...
+    __syncthreads();                // ... and everyone's; nobody reads pair p any more
+  };
+  for (int p = 0; p < npairs; p += 2) {
+    iter(p, std::integral_constant<int, 0>{});
+    if (p + 1 < npairs) iter(p + 1, std::integral_constant<int, 1>{});
+  }
+
+  // dK / dV of this q-head in bf16 (summed over the GQA group by the finalize kernel)
+#pragma unroll
+  for (int db = 0; db < NDB; ++db)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int k = kw + (r & 3) + 8 * (r >> 2) + 4 * hi;
+      if (k < S) {
+        const long off = ((long)b * S + k) * ldo + (long)h * D + db * 32 + l32;
+        dk_part[off] = f2bf(dk[db][r] * scale);
+        dv_part[off] = f2bf(dv[db][r]);
+      }
+    }
+}
+
 // ================================================================== backward dQ (deterministic)
 // Q-major like the forward: per wave 32 query rows, sweep 64-key tiles up to the
 // diagonal; S^T = K Q^T and dP^T = V dO^T (A = K / V rows from LDS, B = Q^T / dO^T
@@ -820,6 +1013,11 @@ struct DqSide {
   hipEvent_t fork = nullptr, join = nullptr;
 };
 
+bool g_dkdv2 = [] {
+  const char* e = std::getenv("FT_FLASH_DKDV2");
+  return e == nullptr || std::atoi(e) != 0;
+}();
+
 bool g_dq_stream = [] {
   const char* e = std::getenv("FT_FLASH_DQ_STREAM");
   return e != nullptr && std::atoi(e) != 0;
@@ -918,6 +1116,11 @@ at::Tensor flash_bwd(const at::Tensor& dout, const at::Tensor& qk, const at::Ten
   // dQ kernel stream: a side stream forked from (and joined back into) the caller's stream
   DqSide* side = det ? dq_side() : nullptr;
   hipStream_t dq_stream = side ? side->stream : ft_stream();
+#define FT_DKDV2(DD)                                                                               \
+  hipLaunchKernelGGL((flash_bwd_dkdv2_kernel<DD>), grid, block, 0, ft_stream(), cptr<bf16_t>(dout),    \
+                     cptr<bf16_t>(qk), cptr<bf16_t>(qkv), cptr<float>(lse), cptr<float>(delta),         \
+                     mptr<bf16_t>(dk_part), mptr<bf16_t>(dv_part), B, (int)S, (int)Hq, (int)Hkv, sl2,    \
+                     scale)
 #define FT_DQ(DD)                                                                                  \
   hipLaunchKernelGGL((flash_bwd_dq_kernel<DD>), dim3(nkt * B * Hq), block, 0, dq_stream,            \
                      cptr<bf16_t>(dout), cptr<bf16_t>(qk), cptr<bf16_t>(qkv), cptr<float>(lse),     \
@@ -930,7 +1133,7 @@ at::Tensor flash_bwd(const at::Tensor& dout, const at::Tensor& qk, const at::Ten
       FT_HIP_CHECK(hipStreamWaitEvent(side->stream, side->fork, 0));
     }
     if (mode == 0) FT_BWD(128, 0);
-    else if (mode == 1) { FT_BWD(128, 1); FT_DQ(128); }
+    else if (mode == 1) { if (g_dkdv2) { FT_DKDV2(128); } else FT_BWD(128, 1); FT_DQ(128); }
     else FT_BWD(128, 2);
   } else {
     hipLaunchKernelGGL(flash_bwd_pre_kernel<64>, dim3(pre_blocks), block, 0, ft_stream(),
@@ -940,7 +1143,7 @@ at::Tensor flash_bwd(const at::Tensor& dout, const at::Tensor& qk, const at::Ten
       FT_HIP_CHECK(hipStreamWaitEvent(side->stream, side->fork, 0));
     }
     if (mode == 0) FT_BWD(64, 0);
-    else if (mode == 1) { FT_BWD(64, 1); FT_DQ(64); }
+    else if (mode == 1) { if (g_dkdv2) { FT_DKDV2(64); } else FT_BWD(64, 1); FT_DQ(64); }
     else FT_BWD(64, 2);
   }
   if (side) {  // everything after (finalize, the caller's later work and frees) follows the dQ kernel
@@ -949,6 +1152,7 @@ at::Tensor flash_bwd(const at::Tensor& dout, const at::Tensor& qk, const at::Ten
     FT_HIP_CHECK(hipStreamWaitEvent(ft_stream(), side->join, 0));
   }
 #undef FT_BWD
+#undef FT_DKDV2
 #undef FT_DQ
   FT_LAUNCH_CHECK();
   const long vec = (long)T * ((Hq + 2 * Hkv) * D / 4);
@@ -962,9 +1166,12 @@ at::Tensor flash_bwd(const at::Tensor& dout, const at::Tensor& qk, const at::Ten
 
 // Same-process A/B switch for the dQ side stream (scripts/ab_step.py).
 void flash_set_dq_stream(bool on) { g_dq_stream = on; }
+// Same-process A/B switch: slice-pair dK/dV kernel vs flash_bwd_kernel<D, 1>.
+void flash_set_dkdv2(bool on) { g_dkdv2 = on; }
 
 TORCH_LIBRARY_FRAGMENT(ftamd, m) {
   m.def("flash_set_dq_stream(bool on) -> ()", &flash_set_dq_stream);
+  m.def("flash_set_dkdv2(bool on) -> ()", &flash_set_dkdv2);
   m.def("flash_fwd(Tensor qk, Tensor qkv, int S, int Hq, int Hkv, int D) -> (Tensor, Tensor)",
         &flash_fwd);
   m.def(

@@ -35,3 +35,8 @@ print(f"fwd {tf:7.1f} us  {2 * unit / tf / 1e6:6.0f} TF/s")
 for mode, name in ((0, "bwd atomics"), (1, "bwd deterministic"), (2, "bwd no-atomic (racy, timing only)")):
     tb = t(lambda: K.flash_bwd(do, qk, qkv, o, lse, S, Hq, Hkv, D, mode))
     print(f"{name:34s} {tb:7.1f} us  {5 * unit / tb / 1e6:6.0f} TF/s (5-matmul count)")
+if hasattr(K, "flash_set_dkdv2"):
+    K.flash_set_dkdv2(False)
+    tb = t(lambda: K.flash_bwd(do, qk, qkv, o, lse, S, Hq, Hkv, D, 1))
+    print(f"{'bwd deterministic, 1-slice dK/dV':34s} {tb:7.1f} us  {5 * unit / tb / 1e6:6.0f} TF/s (5-matmul count)")
+    K.flash_set_dkdv2(True)
