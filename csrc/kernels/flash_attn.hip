@@ -1001,41 +1001,12 @@ __global__ __launch_bounds__(256) void flash_bwd_finalize_kernel(
   }
 }
 
-// Deterministic backward: the dQ kernel and the dK/dV kernel are independent once delta
-// exists, and each ends in a causal tail (the last heavy blocks run on a few CUs). Running
-// the dQ kernel on a second stream lets its blocks fill the CUs the dK/dV tail leaves idle
-// (and vice versa) instead of draining the chip at the kernel boundary.
-// Measured on the 8B step: 0.997x (profiles/r1_flash_dq_stream_ab.log) — the two kernels
-// cannot share a CU (414 + 367 registers per lane), so the overlap is only the tails and
-// the fork/join costs as much. Off by default; FT_FLASH_DQ_STREAM=1 enables it.
-struct DqSide {
-  hipStream_t stream = nullptr;
-  hipEvent_t fork = nullptr, join = nullptr;
-};
-
+// Deterministic backward, dK/dV stage: the slice-pair kernel (default) or the one-slice
+// flash_bwd_kernel<D, 1> (FT_FLASH_DKDV2=0 / flash_set_dkdv2, for A/B).
 bool g_dkdv2 = [] {
   const char* e = std::getenv("FT_FLASH_DKDV2");
   return e == nullptr || std::atoi(e) != 0;
 }();
-
-bool g_dq_stream = [] {
-  const char* e = std::getenv("FT_FLASH_DQ_STREAM");
-  return e != nullptr && std::atoi(e) != 0;
-}();
-
-DqSide* dq_side() {
-  if (!g_dq_stream) return nullptr;
-  static DqSide sides[64];
-  int dev = 0;
-  FT_HIP_CHECK(hipGetDevice(&dev));
-  DqSide& d = sides[dev & 63];
-  if (d.stream == nullptr) {
-    FT_HIP_CHECK(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
-    FT_HIP_CHECK(hipEventCreateWithFlags(&d.fork, hipEventDisableTiming));
-    FT_HIP_CHECK(hipEventCreateWithFlags(&d.join, hipEventDisableTiming));
-  }
-  return &d;
-}
 
 void check_inputs(const at::Tensor& qk, const at::Tensor& qkv, int64_t S, int64_t Hq, int64_t Hkv,
                   int64_t D) {
@@ -1113,43 +1084,27 @@ at::Tensor flash_bwd(const at::Tensor& dout, const at::Tensor& qk, const at::Ten
                      cptr<bf16_t>(qk), cptr<bf16_t>(qkv), cptr<float>(lse), cptr<float>(delta),     \
                      dqp, mptr<bf16_t>(dk_part), mptr<bf16_t>(dv_part), B, (int)S, (int)Hq, (int)Hkv, \
                      sl2, scale)
-  // dQ kernel stream: a side stream forked from (and joined back into) the caller's stream
-  DqSide* side = det ? dq_side() : nullptr;
-  hipStream_t dq_stream = side ? side->stream : ft_stream();
 #define FT_DKDV2(DD)                                                                               \
   hipLaunchKernelGGL((flash_bwd_dkdv2_kernel<DD>), grid, block, 0, ft_stream(), cptr<bf16_t>(dout),    \
                      cptr<bf16_t>(qk), cptr<bf16_t>(qkv), cptr<float>(lse), cptr<float>(delta),         \
                      mptr<bf16_t>(dk_part), mptr<bf16_t>(dv_part), B, (int)S, (int)Hq, (int)Hkv, sl2,    \
                      scale)
 #define FT_DQ(DD)                                                                                  \
-  hipLaunchKernelGGL((flash_bwd_dq_kernel<DD>), dim3(nkt * B * Hq), block, 0, dq_stream,            \
+  hipLaunchKernelGGL((flash_bwd_dq_kernel<DD>), dim3(nkt * B * Hq), block, 0, ft_stream(),          \
                      cptr<bf16_t>(dout), cptr<bf16_t>(qk), cptr<bf16_t>(qkv), cptr<float>(lse),     \
                      cptr<float>(delta), mptr<bf16_t>(dqkv), B, (int)S, (int)Hq, (int)Hkv, sl2, scale)
   if (D == 128) {
     hipLaunchKernelGGL(flash_bwd_pre_kernel<128>, dim3(pre_blocks), block, 0, ft_stream(),
                        cptr<bf16_t>(dout), cptr<bf16_t>(out), mptr<float>(delta), B, (int)S, (int)Hq);
-    if (side) {
-      FT_HIP_CHECK(hipEventRecord(side->fork, ft_stream()));
-      FT_HIP_CHECK(hipStreamWaitEvent(side->stream, side->fork, 0));
-    }
     if (mode == 0) FT_BWD(128, 0);
     else if (mode == 1) { if (g_dkdv2) { FT_DKDV2(128); } else FT_BWD(128, 1); FT_DQ(128); }
     else FT_BWD(128, 2);
   } else {
     hipLaunchKernelGGL(flash_bwd_pre_kernel<64>, dim3(pre_blocks), block, 0, ft_stream(),
                        cptr<bf16_t>(dout), cptr<bf16_t>(out), mptr<float>(delta), B, (int)S, (int)Hq);
-    if (side) {
-      FT_HIP_CHECK(hipEventRecord(side->fork, ft_stream()));
-      FT_HIP_CHECK(hipStreamWaitEvent(side->stream, side->fork, 0));
-    }
     if (mode == 0) FT_BWD(64, 0);
     else if (mode == 1) { if (g_dkdv2) { FT_DKDV2(64); } else FT_BWD(64, 1); FT_DQ(64); }
     else FT_BWD(64, 2);
-  }
-  if (side) {  // everything after (finalize, the caller's later work and frees) follows the dQ kernel
-    FT_LAUNCH_CHECK();
-    FT_HIP_CHECK(hipEventRecord(side->join, side->stream));
-    FT_HIP_CHECK(hipStreamWaitEvent(ft_stream(), side->join, 0));
   }
 #undef FT_BWD
 #undef FT_DKDV2
@@ -1164,13 +1119,10 @@ at::Tensor flash_bwd(const at::Tensor& dout, const at::Tensor& qk, const at::Ten
   return dqkv;
 }
 
-// Same-process A/B switch for the dQ side stream (scripts/ab_step.py).
-void flash_set_dq_stream(bool on) { g_dq_stream = on; }
 // Same-process A/B switch: slice-pair dK/dV kernel vs flash_bwd_kernel<D, 1>.
 void flash_set_dkdv2(bool on) { g_dkdv2 = on; }
 
 TORCH_LIBRARY_FRAGMENT(ftamd, m) {
-  m.def("flash_set_dq_stream(bool on) -> ()", &flash_set_dq_stream);
   m.def("flash_set_dkdv2(bool on) -> ()", &flash_set_dkdv2);
   m.def("flash_fwd(Tensor qk, Tensor qkv, int S, int Hq, int Hkv, int D) -> (Tensor, Tensor)",
         &flash_fwd);

@@ -5,7 +5,7 @@ Knobs toggled between timing windows (alternating rounds, so box and clock drift
   gemm  — TunableOp GEMM solution table (tuning/gemm_gfx950.csv) vs the hipBLASLt heuristic
   dw    — weight-gradient GEMMs on a side stream, concurrent with the dX GEMMs
   prio  — compute on a high-priority stream (its workgroups dispatch ahead of the side streams')
-  dqs   — deterministic flash backward: dQ kernel on a second stream, concurrent with dK/dV
+  dkdv2 — deterministic flash backward: slice-pair dK/dV kernel vs the one-slice kernel
   tonly — SwiGLU kernels write only the transposed activation/gradient; the w2 forward and
           w13 dX GEMMs read them as A^T
 Usage: python scripts/ab_step.py [--steps 8] [--rounds 3] [--configs gemm,dw ...]
@@ -88,7 +88,7 @@ def main():
         torch.cuda.set_stream(hp if on else default_stream)
 
     setters = {"gemm": gemm_tuning.set_enabled, "dw": Fx.set_dw_stream, "tonly": Fx.set_ffn_t_only,
-               "dqs": kernels().flash_set_dq_stream, "prio": set_prio}
+               "dkdv2": kernels().flash_set_dkdv2, "prio": set_prio}
     configs = list(itertools.product([False, True], repeat=len(knobs)))
 
     def apply(cfg):
