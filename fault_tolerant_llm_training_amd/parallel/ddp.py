@@ -41,6 +41,7 @@ and 288 GB of HBM is not the limit for the replicated parameters anyway.
 """
 from __future__ import annotations
 
+import os
 from typing import List, Optional
 
 import torch
@@ -52,6 +53,14 @@ from ..ops.grad_sink import GradSink
 
 MODES = ("local", "allreduce", "zero1")
 PARTIALS_PER_BUCKET = 512
+# A/B switch (scripts/ab_step.py): take every bucket's sum of squares in one pass after
+# backward instead of as each bucket completes (the default overlaps them with backward)
+SUMSQ_AT_END = os.environ.get("FT_SUMSQ_AT_END", "0") == "1"
+
+
+def set_sumsq_at_end(on: bool) -> None:
+    global SUMSQ_AT_END
+    SUMSQ_AT_END = bool(on)
 
 
 class Bucket:
@@ -162,6 +171,7 @@ class GradReducer:
         for sink in list(flat.sinks.values()) + list(extra_sinks):
             sink.hook = self._on_ready
         self.comm = self.world > 1 or mode != "local"
+        self._pending_sumsq: List[Bucket] = []
 
     # ---------------------------------------------------------------- shard views
     def param_shard(self, b: Bucket) -> torch.Tensor:
@@ -249,7 +259,10 @@ class GradReducer:
             if b.work is not None:
                 b.work.wait()  # side stream waits for the collective (host does not)
                 b.work = None
-            self._sumsq(self.grad_for_update(b), b)
+            if SUMSQ_AT_END:
+                self._pending_sumsq.append(b)
+            else:
+                self._sumsq(self.grad_for_update(b), b)
 
     def finish(self) -> None:
         """Launch stragglers; after this, ``partials`` hold every bucket's sum of squares
@@ -261,6 +274,11 @@ class GradReducer:
         for b in self.buckets:
             if not b.launched:
                 self._launch(b)
+        if self._pending_sumsq:  # A/B mode: all partial sums after backward, one pass
+            with torch.cuda.stream(self.side):
+                for b in self._pending_sumsq:
+                    self._sumsq(self.grad_for_update(b), b)
+            self._pending_sumsq = []
         if not self.overlap:
             for b in self.buckets:
                 if b.work is not None:

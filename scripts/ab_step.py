@@ -4,6 +4,7 @@
 Knobs toggled between timing windows (alternating rounds, so box and clock drift cancel):
   gemm  — TunableOp GEMM solution table (tuning/gemm_gfx950.csv) vs the hipBLASLt heuristic
   dw    — weight-gradient GEMMs on a side stream, concurrent with the dX GEMMs
+  sumsq_end — gradient-norm partial sums in one pass after backward instead of during it
   prio  — compute on a high-priority stream (its workgroups dispatch ahead of the side streams')
   dkdv2 — deterministic flash backward: slice-pair dK/dV kernel vs the one-slice kernel
   tonly — SwiGLU kernels write only the transposed activation/gradient; the w2 forward and
@@ -79,6 +80,7 @@ def main():
 
     knobs = [k for k in a.knobs.split(",") if k]
     from fault_tolerant_llm_training_amd._native import kernels
+    from fault_tolerant_llm_training_amd.parallel import ddp as ddp_mod
 
     hp = torch.cuda.Stream(device=dev, priority=-1)
     default_stream = torch.cuda.current_stream(dev)
@@ -88,7 +90,7 @@ def main():
         torch.cuda.set_stream(hp if on else default_stream)
 
     setters = {"gemm": gemm_tuning.set_enabled, "dw": Fx.set_dw_stream, "tonly": Fx.set_ffn_t_only,
-               "dkdv2": kernels().flash_set_dkdv2, "prio": set_prio}
+               "dkdv2": kernels().flash_set_dkdv2, "prio": set_prio, "sumsq_end": ddp_mod.set_sumsq_at_end}
     configs = list(itertools.product([False, True], repeat=len(knobs)))
 
     def apply(cfg):
