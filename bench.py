@@ -46,6 +46,8 @@ def parse():
     ap.add_argument("--device", default="cuda")
     ap.add_argument("--dp-mode", default="", choices=["", "allreduce", "zero1"])
     ap.add_argument("--no-overlap", action="store_true", help="per-bucket optimizer as a serial phase (A/B)")
+    ap.add_argument("--activation-checkpointing", type=int, default=0,
+                    help="recompute this many blocks in backward (-1 = all): long-context runs")
     ap.add_argument("--whole-buffer-optimizer", action="store_true",
                     help="1 GPU: one norm + one AdamW launch over the flat buffer after backward (A/B)")
     return ap.parse_args()
@@ -77,6 +79,8 @@ def main():
 
     margs = model_args_for(a.model, vocab_size=a.vocab_size, seq_len=a.seq_len)
     model = build_model(margs, dev, torch.bfloat16, seed=1234)
+    if a.activation_checkpointing:
+        model.set_activation_checkpointing(a.activation_checkpointing)
     red = GradReducer(model.flat, model.sinks_in_backward_order(), bucket_mb=a.bucket_mb,
                       mode=a.dp_mode or None, overlap=not a.no_overlap)
     if a.whole_buffer_optimizer and world == 1:
@@ -148,7 +152,12 @@ def main():
         "params": model.num_params(),
         "grad_mode": red.mode,
         "buckets": len(red.buckets),
+        "recompute_layers": model.recompute_layers,
     }
+    if dev.type == "cuda":
+        ms_ = torch.cuda.memory_stats(dev)
+        out["hbm_peak_gb"] = round(ms_.get("reserved_bytes.all.peak", 0) / 2**30, 1)
+        out["alloc_retries"] = ms_.get("num_alloc_retries", 0)
     if a.ckpt_dir and not opt.zero1:
         from fault_tolerant_llm_training_amd.ckpt.bench_save import time_checkpoint_save
 

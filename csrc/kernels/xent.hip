@@ -69,22 +69,24 @@ __global__ __launch_bounds__(256) void xent_bwd_kernel(bf16_t* __restrict__ logi
                                                        const float* __restrict__ lse,
                                                        const float* __restrict__ grad,
                                                        const float* __restrict__ inv_count, int V,
-                                                       int ignore_index) {
-  const int row = blockIdx.y;
-  const int64_t y = labels[row];
-  bf16_t* lr = logits + (long)row * V;
-  const float scale = (y == ignore_index) ? 0.f : grad[0] * inv_count[0];
-  const float l = lse[row];
-  for (int c = (blockIdx.x * 256 + threadIdx.x) * 8; c < V; c += gridDim.x * 256 * 8) {
-    float x[8];
-    unpack8(*reinterpret_cast<const uint4*>(lr + c), x);
+                                                       int T, int ignore_index) {
+  // rows grid-strided over y (gridDim.y is capped below 65536; long-context T exceeds it)
+  for (int row = blockIdx.y; row < T; row += gridDim.y) {
+    const int64_t y = labels[row];
+    bf16_t* lr = logits + (long)row * V;
+    const float scale = (y == ignore_index) ? 0.f : grad[0] * inv_count[0];
+    const float l = lse[row];
+    for (int c = (blockIdx.x * 256 + threadIdx.x) * 8; c < V; c += gridDim.x * 256 * 8) {
+      float x[8];
+      unpack8(*reinterpret_cast<const uint4*>(lr + c), x);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      float p = exp2f((x[j] - l) * LOG2E);
-      if (c + j == y) p -= 1.f;
-      x[j] = p * scale;
+      for (int j = 0; j < 8; ++j) {
+        float p = exp2f((x[j] - l) * LOG2E);
+        if (c + j == y) p -= 1.f;
+        x[j] = p * scale;
+      }
+      *reinterpret_cast<uint4*>(lr + c) = pack8(x);
     }
-    *reinterpret_cast<uint4*>(lr + c) = pack8(x);
   }
 }
 
@@ -126,9 +128,9 @@ void xent_bwd_(const at::Tensor& logits, const at::Tensor& labels, const at::Ten
   const at::DeviceGuard guard(logits.device());
   const int bx = std::max(1, std::min((V / 8 + 255) / 256, 8));
   if (T > 0)
-    hipLaunchKernelGGL(xent_bwd_kernel, dim3(bx, T), dim3(256), 0, ft_stream(),
+    hipLaunchKernelGGL(xent_bwd_kernel, dim3(bx, std::min(T, 32768)), dim3(256), 0, ft_stream(),
                        mptr<bf16_t>(logits), cptr<int64_t>(labels), cptr<float>(lse),
-                       cptr<float>(grad), cptr<float>(inv_count), V, (int)ignore_index);
+                       cptr<float>(grad), cptr<float>(inv_count), V, T, (int)ignore_index);
   FT_LAUNCH_CHECK();
 }
 

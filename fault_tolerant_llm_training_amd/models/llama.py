@@ -19,6 +19,7 @@ from dataclasses import dataclass, replace
 from typing import Optional
 
 import torch
+import torch.utils.checkpoint
 import torch.nn as nn
 
 from ..ops import functional as Fx
@@ -165,6 +166,14 @@ class Transformer(nn.Module):
         self.flat: Optional[FlatParamSpace] = None
         self.gate = None  # optim.adamw.ParamGate: per-layer wait for the optimizer's updates
         self._ranges = None
+        self.recompute_layers = 0  # activation checkpointing: blocks [0, n) recompute in backward
+
+    def set_activation_checkpointing(self, n_layers: int) -> None:
+        """Recompute the first ``n_layers`` blocks (-1: all) during backward instead of keeping
+        their activations: only each block's input residual stream stays resident. Costs one
+        extra block forward; extends the reachable sequence length / batch per GPU (SURVEY.md
+        §5.7 — the reference relies on SDPA's O(S) attention memory alone, model.py:212)."""
+        self.recompute_layers = self.n_layers if n_layers < 0 else min(int(n_layers), self.n_layers)
 
     # ------------------------------------------------------------------ materialisation
     def flat_layout(self):
@@ -252,7 +261,12 @@ class Transformer(nn.Module):
         d = None
         for i, layer in enumerate(self.layers.values()):
             self._wait(layer_r[i])
-            h, d = layer(h, d, cos, sin, S)
+            if i < self.recompute_layers and torch.is_grad_enabled():
+                # non-reentrant: the custom Functions' saved tensors are dropped and regenerated
+                # by re-running the block (deterministic kernels → bit-identical gradients)
+                h, d = torch.utils.checkpoint.checkpoint(layer, h, d, cos, sin, S, use_reentrant=False)
+            else:
+                h, d = layer(h, d, cos, sin, S)
         self._wait(final_r)
         a = self.model_args
         ln = a.norm_type == "layernorm"

@@ -16,6 +16,7 @@ LM head model.py:379, loss train.py:101-102.
 """
 from __future__ import annotations
 
+import collections
 import os
 from typing import Optional
 
@@ -48,17 +49,19 @@ def _use_tn(dy2: torch.Tensor, x2: torch.Tensor) -> bool:
 
 
 def weight_grad(dy2: torch.Tensor, x2: torch.Tensor, sink: Optional[GradSink],
-                dyT: Optional[torch.Tensor] = None, xT: Optional[torch.Tensor] = None):
+                dyT: Optional[torch.Tensor] = None, xT: Optional[torch.Tensor] = None, bufs=None):
     """dW[N, K] = dy2[T, N]^T @ x2[T, K], into the sink (flat grad buffer) or returned.
 
     ``dyT`` / ``xT``: already-transposed operands written by a producer kernel (the fused
-    SwiGLU kernels), used instead of running the transpose kernel. ``x2`` may then be None."""
+    SwiGLU kernels), used instead of running the transpose kernel. ``x2`` may then be None.
+    ``bufs``: preallocated (dyT, xT) outputs for the transposes (see weight_grad_async)."""
     if xT is not None and x2 is None:
         x2 = xT.t()
     if _use_tn(dy2, x2):
         K_ = kernels()
-        a = dyT if dyT is not None else K_.transpose2d(dy2.contiguous())   # [N, T]
-        b = xT if xT is not None else K_.transpose2d(x2.contiguous())      # [K, T]
+        ba, bb = bufs if bufs is not None else (None, None)
+        a = dyT if dyT is not None else K_.transpose2d(dy2.contiguous(), ba)   # [N, T]
+        b = xT if xT is not None else K_.transpose2d(x2.contiguous(), bb)      # [K, T]
         if sink is not None:
             sink.mm(a, b.t())
             return None
@@ -79,6 +82,8 @@ def weight_grad(dy2: torch.Tensor, x2: torch.Tensor, sink: Optional[GradSink],
 # FlatAdamW.step) makes the compute stream wait for every dW before the optimizer.
 _DW_STREAM = os.environ.get("FT_DW_STREAM", "1") == "1"
 _dw_streams = {}
+_dw_pending = {}  # device -> FIFO of (dW done event, operands kept alive until then)
+_DW_LAG = int(os.environ.get("FT_DW_LAG", "4"))  # dW GEMMs the compute stream may run ahead by
 
 
 def set_dw_stream(on: bool) -> None:
@@ -105,12 +110,30 @@ def weight_grad_async(dy2: torch.Tensor, x2: Optional[torch.Tensor], sink: Optio
         return weight_grad(dy2, x2, sink, dyT, xT)
     cur = torch.cuda.current_stream(dy2.device)
     side = _dw_side(dy2.device)
+    # Operand lifetime is stream-ordered instead of record_stream(): the operands (and the
+    # transposes' outputs, allocated here on the compute stream) stay referenced in a short
+    # FIFO; before one is dropped the compute stream waits for its dW, so the freed blocks
+    # are reusable by the compute stream at once. record_stream() kept every recorded
+    # activation out of the caching allocator until its event had completed, and with the
+    # host a step ahead of the GPU that held HBM at ~1.6x the allocated peak and sent
+    # long-context steps into allocator cache flushes (profiles/r1_allocator_pools.log).
+    dy2 = dy2.contiguous()
+    x2 = x2.contiguous() if x2 is not None else None
+    xx = x2 if x2 is not None else xT.t()
+    bufs = None
+    if _use_tn(dy2, xx):
+        T, N = dy2.shape
+        bufs = (dy2.new_empty((N, T)) if dyT is None else None,
+                xx.new_empty((xx.shape[1], T)) if xT is None else None)
     side.wait_stream(cur)
     with torch.cuda.stream(side):
-        weight_grad(dy2, x2, sink, dyT, xT)
-    for t in (dy2, x2, dyT, xT):
-        if t is not None:
-            t.record_stream(side)
+        weight_grad(dy2, x2, sink, dyT, xT, bufs)
+        ev = torch.cuda.Event()
+        ev.record()
+    q = _dw_pending.setdefault(_dev_key(dy2.device), collections.deque())
+    q.append((ev, (dy2, x2, dyT, xT, bufs)))
+    while len(q) > _DW_LAG:
+        cur.wait_event(q.popleft()[0])
     return None
 
 
@@ -123,9 +146,13 @@ def join_dw_stream() -> None:
     """Make the current stream wait for all weight gradients issued on the dW side stream."""
     if _dw_streams:
         cur = torch.cuda.current_stream()
-        s = _dw_streams.get(_dev_key(cur.device))
+        k = _dev_key(cur.device)
+        s = _dw_streams.get(k)
         if s is not None:
             cur.wait_stream(s)
+            q = _dw_pending.get(k)
+            if q:
+                q.clear()  # every dW is ordered before the compute stream's next work
 
 
 def _write_weight_grad(sink: Optional[GradSink], g: torch.Tensor):

@@ -176,6 +176,13 @@ def build_parser() -> argparse.ArgumentParser:
         help="Flash-attention backward: atomic-free dQ kernel (bit-reproducible, default) or fp32 atomics",
     )
     parser.add_argument(
+        "--activation-checkpointing",
+        type=int,
+        default=0,
+        help="Recompute this many transformer blocks (from the first; -1 = all) in backward instead of "
+        "storing their activations (long sequences / larger batches per GPU)",
+    )
+    parser.add_argument(
         "--profile-steps",
         type=str,
         default="",

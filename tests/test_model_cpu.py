@@ -106,3 +106,21 @@ def test_layernorm_variant():
     loss.backward()
     assert torch.isfinite(loss)
     assert m.flat.grads.abs().sum() > 0
+
+
+@pytest.mark.parametrize("n", [1, -1])
+def test_activation_checkpointing_same_loss_and_grads(n):
+    """Recomputing blocks in backward (--activation-checkpointing) changes nothing."""
+    a = model_args_for("tiny", vocab_size=128, seq_len=32)
+    tok = torch.randint(0, 128, (2, 32))
+    lab = torch.randint(0, 128, (2, 32))
+    out = []
+    for k in (0, n):
+        m = build_model(a, "cpu", torch.float32, seed=5)
+        m.set_activation_checkpointing(k)
+        loss = m(tok, lab)
+        loss.backward()
+        out.append((loss.detach(), m.flat.grads.clone()))
+    assert m.recompute_layers == (a.n_layers if n < 0 else n)
+    assert torch.equal(out[0][0], out[1][0])
+    assert torch.allclose(out[0][1], out[1][1], rtol=0, atol=1e-6)
