@@ -207,6 +207,164 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(
     *reinterpret_cast<float4*>(part + i) = *reinterpret_cast<const float4*>(red + i);
 }
 
+// Split-row backward: a 1024-thread block = 4 row groups x 4 waves; the 4 waves of a
+// group share one row (wave q owns 512-column chunks q, q+4, ...), so a wave holds
+// CHW = chunks/4 chunks instead of the whole row. The freed registers buy two rows per
+// group in flight (all of a block's 8 rows are requested in one round trip) and 16
+// waves per CU instead of 4 — the one-wave-per-row kernel above spends most of its
+// time waiting on its single round of loads. Row sums cross waves through LDS
+// (double-buffered by iteration parity: one barrier per iteration). dW partials fold
+// in LDS in fixed group order -> one fp32 row per block (deterministic), as above.
+constexpr int SPLIT = 4;    // waves per row
+constexpr int GROUPS = 4;   // row groups per block
+constexpr int RPI = 1;      // rows per group per iteration (loads issued together)
+
+template <int CHW, bool LN>
+__global__ __launch_bounds__(1024) void norm_bwd_split_kernel(
+    const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
+    const float* __restrict__ rstd, const float* __restrict__ mean_in, bf16_t* __restrict__ dx,
+    const bf16_t* __restrict__ dres, float* __restrict__ dw_part, int M, int N,
+    int rows_per_block) {
+  __shared__ float sums[2][GROUPS][RPI][2][SPLIT];  // [parity][group][row][sdnn|sdn][wave]
+  extern __shared__ __attribute__((aligned(16))) float red[];  // [N]
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int q = wave % SPLIT, grp = wave / SPLIT;
+  const int row0 = blockIdx.x * rows_per_block;
+  const uint4 z = make_uint4(0, 0, 0, 0);
+  uint4 wr[CHW];
+  float acc[CHW][8];
+#pragma unroll
+  for (int c = 0; c < CHW; ++c) {
+    const int idx = (c * SPLIT + q) * 512 + lane * 8;
+    wr[c] = idx < N ? *reinterpret_cast<const uint4*>(w + idx) : z;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[c][j] = 0.f;
+  }
+  const float invN = 1.f / (float)N;
+  const int iters = rows_per_block / (GROUPS * RPI);  // block-uniform trip count (barriers)
+  for (int it = 0; it < iters; ++it) {
+    const int par = it & 1;
+    int rows[RPI];
+    uint4 xv[RPI][CHW], gv[RPI][CHW];
+#pragma unroll
+    for (int k = 0; k < RPI; ++k) {
+      const int rr = row0 + (it * RPI + k) * GROUPS + grp;
+      rows[k] = (rr < M && rr < row0 + rows_per_block) ? rr : -1;
+      const size_t off = (size_t)(rows[k] < 0 ? 0 : rows[k]) * N;
+#pragma unroll
+      for (int c = 0; c < CHW; ++c) {
+        const int idx = (c * SPLIT + q) * 512 + lane * 8;
+        const bool ok = rows[k] >= 0 && idx < N;
+        xv[k][c] = ok ? *reinterpret_cast<const uint4*>(x + off + idx) : z;
+        gv[k][c] = ok ? *reinterpret_cast<const uint4*>(dy + off + idx) : z;
+      }
+    }
+    float r[RPI], mu[RPI];
+#pragma unroll
+    for (int k = 0; k < RPI; ++k) {
+      r[k] = rows[k] >= 0 ? rstd[rows[k]] : 0.f;
+      mu[k] = (LN && rows[k] >= 0) ? mean_in[rows[k]] : 0.f;
+      float sdn = 0.f, sdnn = 0.f;
+#pragma unroll
+      for (int c = 0; c < CHW; ++c) {
+        float xf[8], g[8], wf[8];
+        unpack8(xv[k][c], xf);
+        unpack8(gv[k][c], g);
+        unpack8(wr[c], wf);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float n = (xf[j] - mu[k]) * r[k];
+          const float dn = g[j] * wf[j];
+          acc[c][j] += g[j] * n;
+          sdn += dn;
+          sdnn += dn * n;
+        }
+      }
+      sdnn = wave_sum(sdnn);
+      if (LN) sdn = wave_sum(sdn);
+      if (lane == 0) {
+        sums[par][grp][k][0][q] = sdnn;
+        if (LN) sums[par][grp][k][1][q] = sdn;
+      }
+    }
+    __syncthreads();
+    // Opaque to the optimiser: the fp32 unpacks are redone from the packed registers
+    // instead of being kept alive across the barrier (which spilled at 128 VGPRs).
+#pragma unroll
+    for (int k = 0; k < RPI; ++k)
+#pragma unroll
+      for (int c = 0; c < CHW; ++c) {
+        asm volatile("" : "+v"(xv[k][c].x), "+v"(xv[k][c].y), "+v"(xv[k][c].z), "+v"(xv[k][c].w));
+        asm volatile("" : "+v"(gv[k][c].x), "+v"(gv[k][c].y), "+v"(gv[k][c].z), "+v"(gv[k][c].w));
+      }
+#pragma unroll
+    for (int c = 0; c < CHW; ++c)
+      asm volatile("" : "+v"(wr[c].x), "+v"(wr[c].y), "+v"(wr[c].z), "+v"(wr[c].w));
+#pragma unroll
+    for (int k = 0; k < RPI; ++k) {
+      if (rows[k] < 0) continue;
+      float sdnn = 0.f, sdn = 0.f;
+#pragma unroll
+      for (int s = 0; s < SPLIT; ++s) {  // fixed order: every wave of the row gets the same sum
+        sdnn += sums[par][grp][k][0][s];
+        if (LN) sdn += sums[par][grp][k][1][s];
+      }
+      sdnn *= invN;
+      sdn *= invN;
+      bf16_t* dxr = dx + (size_t)rows[k] * N;
+#pragma unroll
+      for (int c = 0; c < CHW; ++c) {
+        const int idx = (c * SPLIT + q) * 512 + lane * 8;
+        if (idx < N) {
+          float xf[8], g[8], wf[8], o[8];
+          unpack8(xv[k][c], xf);
+          unpack8(gv[k][c], g);
+          unpack8(wr[c], wf);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float n = (xf[j] - mu[k]) * r[k];
+            o[j] = r[k] * (g[j] * wf[j] - (LN ? sdn : 0.f) - n * sdnn);
+          }
+          if (dres) {  // loaded after the barrier: keeps the pre-barrier set at 2 operands
+            float rr[8];
+            unpack8(*reinterpret_cast<const uint4*>(dres + (size_t)rows[k] * N + idx), rr);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) o[j] += rr[j];
+          }
+          *reinterpret_cast<uint4*>(dxr + idx) = pack8(o);
+        }
+      }
+    }
+  }
+#pragma unroll 1
+  for (int g = 0; g < GROUPS; ++g) {
+    if (grp == g) {
+#pragma unroll
+      for (int c = 0; c < CHW; ++c) {
+        const int idx = (c * SPLIT + q) * 512 + lane * 8;
+        if (idx < N) {
+          float4* r4 = reinterpret_cast<float4*>(red + idx);
+          if (g == 0) {
+            r4[0] = make_float4(acc[c][0], acc[c][1], acc[c][2], acc[c][3]);
+            r4[1] = make_float4(acc[c][4], acc[c][5], acc[c][6], acc[c][7]);
+          } else {
+            float4 a = r4[0], b = r4[1];
+            a.x += acc[c][0]; a.y += acc[c][1]; a.z += acc[c][2]; a.w += acc[c][3];
+            b.x += acc[c][4]; b.y += acc[c][5]; b.z += acc[c][6]; b.w += acc[c][7];
+            r4[0] = a;
+            r4[1] = b;
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+  float* part = dw_part + (size_t)blockIdx.x * N;
+  for (int i = threadIdx.x * 4; i < N; i += 1024 * 4)
+    *reinterpret_cast<float4*>(part + i) = *reinterpret_cast<const float4*>(red + i);
+}
+
 // Column sums of a [P, N] fp32 slab -> bf16 dw (optionally accumulated).
 // Block = 32 columns x 8 row groups (128-B row segments); fixed summation order
 // (deterministic). 128 blocks for N = 4096.
@@ -247,6 +405,41 @@ void launch_fwd(const bf16_t* x, const bf16_t* d, bf16_t* hout, const bf16_t* w,
   else if (chunks <= 16) FT_NF(16);
   else TORCH_CHECK(false, "norm: N too large");
 #undef FT_NF
+}
+
+// Split-row kernel when every wave owns at least one chunk (N >= 2048) and the LDS
+// fold fits (N <= 8192); FT_NORM_BWD_SPLIT=0 selects the one-wave-per-row kernel (A/B).
+bool use_split_bwd(int N) {
+  const char* e = std::getenv("FT_NORM_BWD_SPLIT");
+  if (e && e[0] == '0') return false;
+  const int chunks = (N + 511) / 512;
+  return chunks >= SPLIT && chunks <= 2 * SPLIT;  // CHW <= 2: no spills at 4 waves/SIMD
+}
+
+// rows per block: a multiple of GROUPS*RPI, at most one block per CU
+void split_grid(int M, int* nblk, int* rows_per_block) {
+  const int unit = GROUPS * RPI;
+  int nb = std::max(1, std::min(256, (M + unit - 1) / unit));
+  int rpb = ((M + nb - 1) / nb + unit - 1) / unit * unit;
+  *rows_per_block = rpb;
+  *nblk = std::max(1, (M + rpb - 1) / rpb);
+}
+
+template <bool LN>
+void launch_bwd_split(const bf16_t* dy, const bf16_t* x, const bf16_t* w, const float* rstd,
+                      const float* mean, bf16_t* dx, const bf16_t* dres, float* part, int nblk,
+                      int rows_per_block, int M, int N, hipStream_t st) {
+  const int chw = ((N + 511) / 512 + SPLIT - 1) / SPLIT;
+  dim3 grid(nblk), block(1024);
+  const size_t lds = (size_t)N * sizeof(float);
+#define FT_NBS(C)                                                                       \
+  hipLaunchKernelGGL((norm_bwd_split_kernel<C, LN>), grid, block, lds, st, dy, x, w, rstd, \
+                     mean, dx, dres, part, M, N, rows_per_block)
+  if (chw <= 1) FT_NBS(1);
+  else if (chw <= 2) FT_NBS(2);
+  else if (chw <= 4) FT_NBS(4);
+  else TORCH_CHECK(false, "norm: N too large for the split kernel");
+#undef FT_NBS
 }
 
 template <bool LN>
@@ -339,8 +532,21 @@ at::Tensor norm_bwd(const at::Tensor& dy, const at::Tensor& x, const at::Tensor&
   }
   // ~2 rows per wave: enough blocks to cover all 256 CUs, few enough partial rows
   int nblk = std::max(1, std::min((M + ROWS_PER_BLOCK * 2 - 1) / (ROWS_PER_BLOCK * 2), 256));
+  const bool split = M > 0 && use_split_bwd(N);
+  int rows_per_block = 0;
+  if (split) split_grid(M, &nblk, &rows_per_block);
   auto part = at::empty({(long)nblk, N}, x.options().dtype(at::kFloat));
-  if (M > 0) {
+  if (split) {
+    if (ln)
+      launch_bwd_split<true>(cptr<bf16_t>(dy), cptr<bf16_t>(x), cptr<bf16_t>(w), cptr<float>(rstd),
+                             cptr<float>(*mean), mptr<bf16_t>(dx), dr, mptr<float>(part), nblk,
+                             rows_per_block, M, N, ft_stream());
+    else
+      launch_bwd_split<false>(cptr<bf16_t>(dy), cptr<bf16_t>(x), cptr<bf16_t>(w), cptr<float>(rstd),
+                              nullptr, mptr<bf16_t>(dx), dr, mptr<float>(part), nblk,
+                              rows_per_block, M, N, ft_stream());
+    FT_LAUNCH_CHECK();
+  } else if (M > 0) {
     if (ln)
       launch_bwd<true>(cptr<bf16_t>(dy), cptr<bf16_t>(x), cptr<bf16_t>(w), cptr<float>(rstd),
                        cptr<float>(*mean), mptr<bf16_t>(dx), dr, mptr<float>(part), nblk, M, N,

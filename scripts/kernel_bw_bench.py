@@ -54,6 +54,10 @@ case("add_norm_fwd [2048x4096]", lambda: K.add_norm_fwd(x, d, w, 1e-5, False), 4
 dy, dres, dw = r(T, D), r(T, D), torch.empty(D, device="cuda").bfloat16()
 case("norm_bwd (+residual grad) [2048x4096]", lambda: K.norm_bwd(dy, h, w, rstd, None, dw, dres, False),
      4 * T * D * 2)
+os.environ["FT_NORM_BWD_SPLIT"] = "0"  # A/B: the one-wave-per-row kernel
+case("norm_bwd 1-wave-per-row (A/B)", lambda: K.norm_bwd(dy, h, w, rstd, None, dw, dres, False), 4 * T * D * 2)
+os.environ.pop("FT_NORM_BWD_SPLIT")
+case("norm_bwd split-row (again)", lambda: K.norm_bwd(dy, h, w, rstd, None, dw, dres, False), 4 * T * D * 2)
 gu = r(T, 2 * F)
 case("swiglu_fwd_t (a + a^T) [2048x14336]", lambda: K.swiglu_fwd_t(gu), (2 * T * F + 2 * T * F) * 2)
 da = r(T, F)

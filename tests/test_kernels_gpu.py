@@ -20,7 +20,7 @@ def rel(a, b):
     return ((a - b).norm() / (b.norm() + 1e-12)).item()
 
 
-@pytest.mark.parametrize("M,N", [(1, 128), (7, 768), (2048, 4096), (33, 1024), (5, 8192)])
+@pytest.mark.parametrize("M,N", [(1, 128), (7, 768), (2048, 4096), (33, 1024), (5, 8192), (300, 2560), (4099, 2048)])
 @pytest.mark.parametrize("ln", [False, True])
 def test_norm(K, M, N, ln):
     torch.manual_seed(0)
