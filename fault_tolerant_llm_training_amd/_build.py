@@ -158,11 +158,45 @@ def build(jobs: int = 0, force: bool = False, verbose: bool = True) -> None:
                 print(f"[build] linked {out.relative_to(ROOT)}", flush=True)
 
 
+SANITIZERS = {"asan": ["address", "undefined"], "tsan": ["thread"]}
+SELFTEST_SRCS = ("signals.cpp", "zip_writer.cpp", "file_reader.cpp")
+
+
+def build_selftest(kind: str, out_dir: Path = None, verbose: bool = False) -> Path:
+    """Host-only build of csrc/tests/runtime_selftest.cpp + the runtime's host sources under
+    ASan+UBSan (``asan``) or ThreadSanitizer (``tsan``) — SURVEY.md §5.2. Each ``-fsanitize=``
+    follows ``-Xarch_host`` so only host code is instrumented (no GPU sanitizer on this pool);
+    the sources are compiled as plain C++ (no device code in them)."""
+    out_dir = Path(out_dir or (BUILD / f"selftest_{kind}"))
+    out_dir.mkdir(parents=True, exist_ok=True)
+    san = []
+    for name in SANITIZERS[kind]:
+        san += ["-Xarch_host", f"-fsanitize={name}"]
+    flags = ["-O1", "-g", "-std=c++17", "-fno-omit-frame-pointer", "-D__HIP_PLATFORM_AMD__=1",
+             "-I", str(CSRC / "runtime"), *san]
+    if kind == "asan":
+        flags += ["-Xarch_host", "-fno-sanitize-recover=undefined"]
+    srcs = [CSRC / "runtime" / f for f in SELFTEST_SRCS] + [CSRC / "tests" / "runtime_selftest.cpp"]
+    exe = out_dir / "runtime_selftest"
+    cmd = [_hipcc(), *flags, *map(str, srcs), "-L/opt/rocm/lib", "-lamdhip64", "-lz", "-lpthread",
+           "-Wl,-rpath,/opt/rocm/lib", "-o", str(exe)]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"selftest build failed ({kind})\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    if verbose:
+        print(f"[build] {exe}", flush=True)
+    return exe
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("-j", "--jobs", type=int, default=0)
     ap.add_argument("--force", action="store_true")
+    ap.add_argument("--selftest", choices=sorted(SANITIZERS), help="build the sanitized runtime self-test")
     a = ap.parse_args(argv)
+    if a.selftest:
+        build_selftest(a.selftest, verbose=True)
+        return 0
     build(a.jobs, a.force)
 
 
