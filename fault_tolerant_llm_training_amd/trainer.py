@@ -267,6 +267,11 @@ def train(args) -> int:
                     mode=args.checkpoint_mode, writer_threads=args.checkpoint_writer_threads)
         return ckpt["engine"]
 
+    if not args.no_checkpoint_prealloc:
+        # pin the snapshot's host buffers while training starts: the first save (often the
+        # SIGUSR1 one, racing the Slurm deadline) then only copies and writes
+        ckpt_engine().preallocate_async()
+
     def save_checkpoint(blocking: bool, collective: bool = True):
         optimizer.gate.wait_all()  # the snapshot must follow this step's parameter updates
         if collective:

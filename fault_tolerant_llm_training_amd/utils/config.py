@@ -138,6 +138,11 @@ def build_parser() -> argparse.ArgumentParser:
         "straight into pinned host memory; auto = hbm when free HBM allows",
     )
     parser.add_argument(
+        "--no-checkpoint-prealloc",
+        action="store_true",
+        help="Pin the checkpoint host buffers at the first save instead of in a background thread at startup",
+    )
+    parser.add_argument(
         "--checkpoint-writer-threads", type=int, default=8, help="Parallel pwrite threads of the checkpoint writer"
     )
     parser.add_argument(

@@ -174,3 +174,17 @@ def test_file_backing_of_mmap_checkpoint(tmp_path):
         raw = f.read(t.numel() * 4)
     assert torch.equal(torch.frombuffer(bytearray(raw), dtype=torch.float32), t)
     assert file_backing(torch.randn(100)) is None
+
+
+def test_background_preallocation_cpu(tmp_path):
+    m, opt, s = _setup()
+    eng = _engine(m, opt)
+    eng.preallocate_async()
+    assert eng.preallocated(30)
+    host = eng.host_views()
+    path = checkpoint_file(str(tmp_path / "ck"), 9)
+    eng.save(path, lambda h: build_checkpoint(m, opt, s, 2, h), step=2, blocking=True)
+    assert eng.host_views() is host  # the save reused the preallocated buffers
+    c = torch.load(path, map_location="cpu", weights_only=True)
+    for k, v in m.state_dict().items():
+        assert torch.equal(c["model"][k], v), k

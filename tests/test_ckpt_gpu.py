@@ -30,3 +30,26 @@ def test_snapshot_engine_roundtrip_and_fence(tmp_path, mode):
     assert torch.equal(c["model"]["p"], ref["params"].cpu())
     assert torch.equal(c["m"], ref["exp_avg"].cpu()) and torch.equal(c["v"], ref["exp_avg_sq"].cpu())
     assert c["training_step"] == 3
+
+
+def test_background_pinned_preallocation(tmp_path):
+    """Pinned host buffers allocated by a background thread at startup; "auto" mode is decided
+    at the first save, so the early engine reserves no HBM staging copy."""
+    from fault_tolerant_llm_training_amd.ckpt.engine import CheckpointEngine
+    from fault_tolerant_llm_training_amd.ckpt.format import load_checkpoint
+
+    n = 5 * (1 << 20) + 8
+    bufs = {k: torch.randn(n, device="cuda").bfloat16() for k in ("params", "exp_avg", "exp_avg_sq")}
+    eng = CheckpointEngine(bufs, mode="auto")
+    before = torch.cuda.memory_allocated()
+    eng.preallocate_async()
+    assert torch.cuda.memory_allocated() == before  # no staging copy yet
+    assert eng._mode == "auto"
+    path = str(tmp_path / "p.ckpt")
+    # the save may race the thread: it blocks on the host-buffer lock, then uses the same buffers
+    st = eng.save(path, lambda h: {"m": h["params"], "a": h["exp_avg"], "v": h["exp_avg_sq"]}, blocking=True)
+    assert eng.preallocated(0) and eng.prealloc_s is not None
+    assert eng.mode in ("hbm", "host") and st.mode == eng.mode
+    assert all(t.is_pinned() for t in eng.host_views().values())
+    c = load_checkpoint(path)
+    assert torch.equal(c["m"], bufs["params"].cpu()) and torch.equal(c["v"], bufs["exp_avg_sq"].cpu())
