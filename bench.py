@@ -152,6 +152,11 @@ def main():
         "params": model.num_params(),
         "grad_mode": red.mode,
         "buckets": len(red.buckets),
+        # bytes each rank sends (and receives) per step in the gradient/parameter collectives:
+        # reduce-scatter + all-gather (ZeRO-1) or all-reduce, 2(W-1)/W of the dense gradient
+        "comm_GB_per_rank_per_step": round(
+            2.0 * (world - 1) / world * sum(b.numel for b in red.buckets if not b.sparse)
+            * model.flat.grads.element_size() / 1e9, 2),
         "recompute_layers": model.recompute_layers,
     }
     if dev.type == "cuda":
