@@ -508,19 +508,24 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> norm_fwd(const at::Tensor& x, con
 
 // Returns dx; writes (or accumulates) dw into `dw` (a view into the flat grad buffer).
 // `dres` (optional) is added into dx: the residual-stream gradient fused into the norm.
-at::Tensor norm_bwd(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& w,
-                    const at::Tensor& rstd, const std::optional<at::Tensor>& mean,
-                    const at::Tensor& dw, const std::optional<at::Tensor>& dres,
-                    bool accumulate) {
+// dx and the per-block fp32 dW partial rows [P, N]; colsum_ folds them into dw. Split so
+// the fold can run on the weight-gradient stream (ops/functional.py): during backward the
+// compute stream shares the CUs with the dW GEMMs and every small launch on it waits for
+// CU slots, so the fold does not belong on the critical path.
+std::tuple<at::Tensor, at::Tensor> norm_bwd_part(const at::Tensor& dy, const at::Tensor& x,
+                                                 const at::Tensor& w, const at::Tensor& rstd,
+                                                 const std::optional<at::Tensor>& mean,
+                                                 const std::optional<at::Tensor>& dres) {
   FT_CHECK_CUDA(dy);
   FT_CHECK_BF16(dy);
   FT_CHECK_CONTIG(dy);
   FT_CHECK_CONTIG(x);
-  FT_CHECK_BF16(dw);
-  FT_CHECK_CONTIG(dw);
+  FT_CHECK_BF16(w);
+  FT_CHECK_CONTIG(w);
   const int N = x.size(-1);
   const int M = x.numel() / N;
-  TORCH_CHECK(dy.numel() == x.numel() && dw.numel() == N, "norm_bwd: shape mismatch");
+  TORCH_CHECK(dy.numel() == x.numel() && w.numel() == N, "norm_bwd: shape mismatch");
+  TORCH_CHECK(N <= 8192 && N % 8 == 0, "norm_bwd: N must be a multiple of 8 and <= 8192");
   const at::DeviceGuard guard(x.device());
   auto dx = at::empty_like(x);
   const bool ln = mean.has_value() && mean->defined() && mean->numel() > 0;
@@ -557,10 +562,32 @@ at::Tensor norm_bwd(const at::Tensor& dy, const at::Tensor& x, const at::Tensor&
                         ft_stream());
     FT_LAUNCH_CHECK();
   }
+  return {dx, M > 0 ? part : part.narrow(0, 0, 0)};
+}
+
+// dw (bf16, [N]) = column sums of part [P, N] (+ dw when accumulating); fixed order.
+void colsum_(const at::Tensor& part, const at::Tensor& dw, bool accumulate) {
+  FT_CHECK_CUDA(part);
+  FT_CHECK_CONTIG(part);
+  FT_CHECK_BF16(dw);
+  FT_CHECK_CONTIG(dw);
+  TORCH_CHECK(part.scalar_type() == at::kFloat && part.dim() == 2 && part.size(1) == dw.numel(),
+              "colsum_: part must be fp32 [P, N] with N = dw.numel()");
+  const at::DeviceGuard guard(dw.device());
+  const int N = dw.numel();
   hipLaunchKernelGGL(colsum_kernel, dim3((N + 31) / 32), dim3(256), 0, ft_stream(),
-                     cptr<float>(part), mptr<bf16_t>(dw), M > 0 ? nblk : 0, N, accumulate);
+                     cptr<float>(part), mptr<bf16_t>(dw), (int)part.size(0), N, accumulate);
   FT_LAUNCH_CHECK();
-  return dx;
+}
+
+at::Tensor norm_bwd(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& w,
+                    const at::Tensor& rstd, const std::optional<at::Tensor>& mean,
+                    const at::Tensor& dw, const std::optional<at::Tensor>& dres,
+                    bool accumulate) {
+  TORCH_CHECK(dw.numel() == w.numel(), "norm_bwd: dw shape mismatch");
+  auto r = norm_bwd_part(dy, x, w, rstd, mean, dres);
+  colsum_(std::get<1>(r), dw, accumulate);
+  return std::get<0>(r);
 }
 
 TORCH_LIBRARY_FRAGMENT(ftamd, m) {
@@ -570,6 +597,11 @@ TORCH_LIBRARY_FRAGMENT(ftamd, m) {
       "add_norm_fwd(Tensor x, Tensor? d, Tensor w, float eps, bool layernorm) -> (Tensor, Tensor, "
       "Tensor, Tensor)",
       &add_norm_fwd);
+  m.def(
+      "norm_bwd_part(Tensor dy, Tensor x, Tensor w, Tensor rstd, Tensor? mean, Tensor? dres) -> "
+      "(Tensor, Tensor)",
+      &norm_bwd_part);
+  m.def("colsum_(Tensor part, Tensor(a!) dw, bool accumulate) -> ()", &colsum_);
   m.def(
       "norm_bwd(Tensor dy, Tensor x, Tensor w, Tensor rstd, Tensor? mean, Tensor(a!) dw, "
       "Tensor? dres, bool accumulate) -> Tensor",

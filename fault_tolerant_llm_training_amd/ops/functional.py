@@ -155,6 +155,32 @@ def join_dw_stream() -> None:
                 q.clear()  # every dW is ordered before the compute stream's next work
 
 
+# A/B (FT_NORM_FOLD_SIDE=1): the norm weight gradient's column fold on the dW side stream
+# instead of the compute stream — during backward the compute stream shares the CUs with the
+# dW GEMMs and each small kernel on it waits for CU slots, while the fold is only needed by
+# the optimizer. Measured 108.0 / 108.1 / 109.0 vs 108.2 / 108.0 / 107.8 ms (off):
+# no gain, so off by default (profiles/r1_norm_fold_side_ab.log).
+_NORM_FOLD_SIDE = os.environ.get("FT_NORM_FOLD_SIDE", "0") == "1"
+
+
+def norm_bwd_into_sink(dy, x, w, rstd, mean, sink: GradSink, dres=None) -> torch.Tensor:
+    """dx of the (add-)norm backward; dW folded into ``sink`` (then ``sink.ready()``)."""
+    K_ = kernels()
+    if not (_NORM_FOLD_SIDE and _DW_STREAM):
+        dx = K_.norm_bwd(dy, x, w, rstd, mean, sink.buf, dres, sink.accumulate)
+        sink.ready()
+        return dx
+    dx, part = K_.norm_bwd_part(dy, x, w, rstd, mean, dres)
+    cur = torch.cuda.current_stream(dy.device)
+    side = _dw_side(dy.device)
+    side.wait_stream(cur)
+    with torch.cuda.stream(side):
+        K_.colsum_(part, sink.buf, sink.accumulate)
+    part.record_stream(side)  # 4 MB of partial sums: the allocator keeps it until the fold ran
+    sink.ready()  # the bucket's work is issued from the dW stream, after the fold
+    return dx
+
+
 def _write_weight_grad(sink: Optional[GradSink], g: torch.Tensor):
     """CPU helper: route a computed weight gradient into its sink (or return it)."""
     if sink is None:
@@ -231,9 +257,7 @@ class NormFn(torch.autograd.Function):
         if dy.is_cuda:
             x, w, rstd, mean = ctx.saved_tensors
             if sink is not None:
-                dx = kernels().norm_bwd(dy.contiguous(), x, w, rstd, mean, sink.buf, None, sink.accumulate)
-                sink.ready()
-                return dx, None, None, None, None
+                return norm_bwd_into_sink(dy.contiguous(), x, w, rstd, mean, sink), None, None, None, None
             dw = torch.empty_like(w)
             dx = kernels().norm_bwd(dy.contiguous(), x, w, rstd, mean, dw, None, False)
             return dx, dw, None, None, None
@@ -274,12 +298,11 @@ class AddNormFn(torch.autograd.Function):
         if dy.is_cuda:
             h, w, rstd, mean = ctx.saved_tensors
             dres = dh.contiguous() if dh is not None else None
-            buf = sink.buf if sink is not None else torch.empty_like(w)
-            g = kernels().norm_bwd(dy.contiguous(), h, w, rstd, mean, buf, dres,
-                                   sink.accumulate if sink is not None else False)
             if sink is not None:
-                sink.ready()
+                g = norm_bwd_into_sink(dy.contiguous(), h, w, rstd, mean, sink, dres)
                 return g, g, None, None, None, None
+            buf = torch.empty_like(w)
+            g = kernels().norm_bwd(dy.contiguous(), h, w, rstd, mean, buf, dres, False)
             return g, g, buf, None, None, None
         h, w = ctx.saved_tensors
         with torch.enable_grad():
