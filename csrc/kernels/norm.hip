@@ -519,18 +519,24 @@ std::tuple<at::Tensor, at::Tensor> norm_bwd_part(const at::Tensor& dy, const at:
   FT_CHECK_CUDA(dy);
   FT_CHECK_BF16(dy);
   FT_CHECK_CONTIG(dy);
+  FT_CHECK_CUDA(x);
+  FT_CHECK_BF16(x);
   FT_CHECK_CONTIG(x);
   FT_CHECK_BF16(w);
   FT_CHECK_CONTIG(w);
+  FT_CHECK_F32(rstd);
+  FT_CHECK_CONTIG(rstd);
   const int N = x.size(-1);
   const int M = x.numel() / N;
   TORCH_CHECK(dy.numel() == x.numel() && w.numel() == N, "norm_bwd: shape mismatch");
+  TORCH_CHECK(rstd.numel() == M, "norm_bwd: rstd must hold one value per row");
   TORCH_CHECK(N <= 8192 && N % 8 == 0, "norm_bwd: N must be a multiple of 8 and <= 8192");
   const at::DeviceGuard guard(x.device());
   auto dx = at::empty_like(x);
   const bool ln = mean.has_value() && mean->defined() && mean->numel() > 0;
   const bf16_t* dr = nullptr;
   if (dres.has_value() && dres->defined()) {
+    FT_CHECK_BF16((*dres));
     FT_CHECK_CONTIG((*dres));
     TORCH_CHECK(dres->numel() == x.numel(), "norm_bwd: dres shape mismatch");
     dr = cptr<bf16_t>(*dres);

@@ -118,7 +118,11 @@ __global__ __launch_bounds__(1024) void norm_finish_kernel(const float* __restri
     stats[0] = norm;
     const bool bad = !isfinite(norm);
     stats[1] = (max_norm > 0.f && !bad) ? fminf(1.f, max_norm / (norm + 1e-6f)) : 1.f;
-    stats[2] = bad ? 1.f : 0.f;
+    // sticky: once a step's norm was non-finite every later update is skipped too, until
+    // the host clears stats[2] (it only does so on an explicit reset). The trainer detects a
+    // bad step two steps late without a host sync and rolls the counters back to it; the
+    // parameters/moments are still exactly those before the bad step.
+    stats[2] = (bad || stats[2] != 0.f) ? 1.f : 0.f;
   }
 }
 

@@ -9,7 +9,11 @@
 namespace py = pybind11;
 using namespace ftrt;
 
-static torch::Tensor pinned_empty(uint64_t nbytes) {
+// Runs without the GIL (the background prealloc thread pins 16-48 GB while the training
+// thread keeps running). `device` >= 0 is made current in the calling thread first: HIP's
+// current device is per thread, and the pinned pages should belong to this rank's GPU.
+static torch::Tensor pinned_empty(uint64_t nbytes, int device) {
+  if (device >= 0 && hipSetDevice(device) != hipSuccess) throw std::runtime_error("hipSetDevice failed");
   uintptr_t p = pinned_alloc(nbytes);
   return torch::from_blob(
       reinterpret_cast<void*>(p), {(int64_t)nbytes},
@@ -75,7 +79,8 @@ PYBIND11_MODULE(_runtime, m) {
       .def("query", &SnapshotEngine::query)
       .def("sync", &SnapshotEngine::sync, py::call_guard<py::gil_scoped_release>())
       .def("event_handle", &SnapshotEngine::event_handle)
-      .def("stream_handle", &SnapshotEngine::stream_handle);
+      .def("stream_handle", &SnapshotEngine::stream_handle)
+      .def("num_events", &SnapshotEngine::num_events);
 
   m.def("write_pieces", &write_pieces, py::arg("path"), py::arg("file_offs"), py::arg("ptrs"), py::arg("lens"),
         py::arg("nthreads") = 8, py::arg("wait_event") = 0, py::arg("fsync") = true, py::arg("direct") = true,
@@ -90,5 +95,7 @@ PYBIND11_MODULE(_runtime, m) {
       .def_property_readonly("bytes", &FileReader::bytes)
       .def_property_readonly("direct_bytes", &FileReader::direct_bytes);
   m.def("cu_mask_stream", &cu_mask_stream, py::arg("device"), py::arg("mask"));
-  m.def("pinned_empty", &pinned_empty, "Exact-size pinned host buffer (hipHostMalloc) as a uint8 tensor");
+  m.def("pinned_empty", &pinned_empty, py::arg("nbytes"), py::arg("device") = -1,
+        py::call_guard<py::gil_scoped_release>(),
+        "Exact-size pinned host buffer (hipHostMalloc) as a uint8 tensor");
 }

@@ -141,9 +141,13 @@ class SnapshotEngine {
   void sync(int ev);
   uintptr_t event_handle(int ev);
   uintptr_t stream_handle();
+  int num_events();  // events created so far (a fixed pool: reused by every save)
 
  private:
+  static constexpr int kPool = 8;
+  int next_event();
   int device_;
+  int next_ = 0;
   void* stream_ = nullptr;
   std::vector<void*> events_;
   std::mutex mu_;

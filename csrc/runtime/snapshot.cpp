@@ -31,14 +31,26 @@ SnapshotEngine::~SnapshotEngine() {
   if (stream_) hipStreamDestroy(reinterpret_cast<hipStream_t>(stream_));
 }
 
+// Events are a small pool reused by every save: a save starts only after the previous
+// one is durable (CheckpointEngine.save waits for it), so its begin() may re-record slot 0
+// and its mark()s the next slots; a long --save-every run creates at most kPool events.
+int SnapshotEngine::next_event() {
+  if (next_ >= (int)events_.size()) {
+    if ((int)events_.size() >= kPool) throw std::runtime_error("SnapshotEngine: too many events in one save");
+    hipEvent_t e;
+    check(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
+    events_.push_back(e);
+  }
+  return next_++;
+}
+
 void SnapshotEngine::begin(uintptr_t compute_stream) {
   std::lock_guard<std::mutex> g(mu_);
   check(hipSetDevice(device_), "hipSetDevice");
-  hipEvent_t e;
-  check(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
+  next_ = 0;
+  hipEvent_t e = reinterpret_cast<hipEvent_t>(events_[next_event()]);  // slot 0
   check(hipEventRecord(e, reinterpret_cast<hipStream_t>(compute_stream)), "hipEventRecord");
   check(hipStreamWaitEvent(reinterpret_cast<hipStream_t>(stream_), e, 0), "hipStreamWaitEvent");
-  events_.push_back(e);
 }
 
 void SnapshotEngine::copy(uintptr_t dst, uintptr_t src, uint64_t nbytes) {
@@ -56,12 +68,13 @@ void SnapshotEngine::copy(uintptr_t dst, uintptr_t src, uint64_t nbytes) {
 
 int SnapshotEngine::mark() {
   std::lock_guard<std::mutex> g(mu_);
-  hipEvent_t e;
-  check(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
-  check(hipEventRecord(e, reinterpret_cast<hipStream_t>(stream_)), "hipEventRecord");
-  events_.push_back(e);
-  return (int)events_.size() - 1;
+  const int i = next_event();
+  check(hipEventRecord(reinterpret_cast<hipEvent_t>(events_[i]), reinterpret_cast<hipStream_t>(stream_)),
+        "hipEventRecord");
+  return i;
 }
+
+int SnapshotEngine::num_events() { return (int)events_.size(); }
 
 void SnapshotEngine::stream_wait(uintptr_t compute_stream, int ev) {
   check(hipStreamWaitEvent(reinterpret_cast<hipStream_t>(compute_stream),

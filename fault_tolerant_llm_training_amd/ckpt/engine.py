@@ -174,7 +174,8 @@ class CheckpointEngine:
             for k, b in self.buffers.items():
                 nb = b.numel() * b.element_size()
                 if self.is_cuda and self.native:
-                    raw = runtime().pinned_empty(nb)  # exact size (torch's pinned pool rounds to 2^k)
+                    # exact size (torch's pinned pool rounds to 2^k), pinned for this rank's GPU
+                    raw = runtime().pinned_empty(nb, self.device.index or 0)
                 elif self.is_cuda:
                     raw = torch.empty(nb, dtype=torch.uint8, pin_memory=True)
                 else:
@@ -206,6 +207,8 @@ class CheckpointEngine:
 
         def run():
             t0 = time.perf_counter()
+            if self.is_cuda:
+                torch.cuda.set_device(self.device)  # per-thread current device (pinned-page placement)
             self._ensure_host()
             self.prealloc_s = time.perf_counter() - t0
 

@@ -65,27 +65,31 @@ def resubmit(script: str, job_id: Optional[str], logger) -> bool:
 
 
 def handle_exit(save_checkpoint: Callable[[], object], training_step: int, exit_type: int, logger,
-                job_id: Optional[str] = None, sbatch_script: str = "", is_main: bool = True) -> None:
+                job_id: Optional[str] = None, sbatch_script: str = "", is_main: bool = True,
+                rank: int = 0) -> None:
     """Apply the exit policy.
 
     ``save_checkpoint()`` writes the checkpoint durably (blocking); it is called on
-    every rank (the engine decides which ranks write). Only the main rank logs
-    and resubmits.
+    every rank (the engine decides which ranks write). Only the main rank resubmits.
+    The main rank logs the reference's lines; every other rank (which logs at WARNING
+    only) reports the same lines once, prefixed with its rank, so a job log shows
+    that all ranks stopped and saved at the same step.
     """
+    say = logger.info if is_main else (lambda m: logger.warning(f"[rank {rank}] {m}"))
     if exit_type == SIGTERM:
-        logger.info("[EXIT HANDLER] Job cancelled, terminating.")
+        say("[EXIT HANDLER] Job cancelled, terminating.")
         return
     if exit_type == SIGUSR1:
-        logger.info("[EXIT HANDLER] Job timed out, saving checkpoint.")
+        say("[EXIT HANDLER] Job timed out, saving checkpoint.")
     elif exit_type == ERROR:
-        logger.info("[EXIT HANDLER] Error during training encountered, saving checkpoint.")
+        say("[EXIT HANDLER] Error during training encountered, saving checkpoint.")
     else:
-        logger.info(f"[EXIT HANDLER] Unknown exit signal {exit_type}, terminating.")
+        say(f"[EXIT HANDLER] Unknown exit signal {exit_type}, terminating.")
         return
     if save_checkpoint() is False:
         logger.error(f"[EXIT HANDLER] Checkpoint could not be saved at step {training_step}")
         return
-    logger.info(f"[EXIT HANDLER] Checkpoint saved at step {training_step}")
+    say(f"[EXIT HANDLER] Checkpoint saved at step {training_step}")
     if exit_type == SIGUSR1 and is_main:
         script = sbatch_script or os.path.join(os.getenv("WORKDIR", ""), "train.sh")
         if not resubmit(script, job_id, logger):

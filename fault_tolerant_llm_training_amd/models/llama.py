@@ -177,13 +177,16 @@ class Transformer(nn.Module):
 
     # ------------------------------------------------------------------ materialisation
     def flat_layout(self):
-        """Flat-buffer order: embedding, per layer [wq wk wv | wo | w1 w3 | w2 | norms], head."""
+        """Flat-buffer order: embedding, per layer [attention_norm | wq wk wv | wo | ffn_norm |
+        w1 w3 | w2], head. Within a layer this is forward order, so backward produces the
+        gradients at strictly descending addresses and the reducer's buckets (cut from the
+        top down, launched in order) complete one after another."""
         names = ["tok_embeddings.weight"]
         for i in range(self.n_layers):
             p = f"layers.{i}."
-            names += [p + "attention.wq.weight", p + "attention.wk.weight", p + "attention.wv.weight",
-                      p + "attention.wo.weight", p + "feed_forward.w1.weight", p + "feed_forward.w3.weight",
-                      p + "feed_forward.w2.weight", p + "attention_norm.weight", p + "ffn_norm.weight"]
+            names += [p + "attention_norm.weight", p + "attention.wq.weight", p + "attention.wk.weight",
+                      p + "attention.wv.weight", p + "attention.wo.weight", p + "ffn_norm.weight",
+                      p + "feed_forward.w1.weight", p + "feed_forward.w3.weight", p + "feed_forward.w2.weight"]
         names += ["norm.weight", "output.weight"]
         return names
 
@@ -286,10 +289,6 @@ class Transformer(nn.Module):
 
 
 def build_model(args: TransformerModelArgs, device, dtype=torch.bfloat16, seed: int = 1234) -> Transformer:
-    if torch.device(device).type == "cuda":
-        from ..ops.gemm_tuning import use_tuned_gemms
-
-        use_tuned_gemms()  # per-shape hipBLASLt/rocBLAS solutions (tuning/gemm_gfx950.csv), if present
     return Transformer(args).materialize(device, dtype, seed)
 
 

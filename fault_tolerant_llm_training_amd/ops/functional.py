@@ -155,29 +155,12 @@ def join_dw_stream() -> None:
                 q.clear()  # every dW is ordered before the compute stream's next work
 
 
-# A/B (FT_NORM_FOLD_SIDE=1): the norm weight gradient's column fold on the dW side stream
-# instead of the compute stream — during backward the compute stream shares the CUs with the
-# dW GEMMs and each small kernel on it waits for CU slots, while the fold is only needed by
-# the optimizer. Measured 108.0 / 108.1 / 109.0 vs 108.2 / 108.0 / 107.8 ms (off):
-# no gain, so off by default (profiles/r1_norm_fold_side_ab.log).
-_NORM_FOLD_SIDE = os.environ.get("FT_NORM_FOLD_SIDE", "0") == "1"
-
-
 def norm_bwd_into_sink(dy, x, w, rstd, mean, sink: GradSink, dres=None) -> torch.Tensor:
-    """dx of the (add-)norm backward; dW folded into ``sink`` (then ``sink.ready()``)."""
-    K_ = kernels()
-    if not (_NORM_FOLD_SIDE and _DW_STREAM):
-        dx = K_.norm_bwd(dy, x, w, rstd, mean, sink.buf, dres, sink.accumulate)
-        sink.ready()
-        return dx
-    dx, part = K_.norm_bwd_part(dy, x, w, rstd, mean, dres)
-    cur = torch.cuda.current_stream(dy.device)
-    side = _dw_side(dy.device)
-    side.wait_stream(cur)
-    with torch.cuda.stream(side):
-        K_.colsum_(part, sink.buf, sink.accumulate)
-    part.record_stream(side)  # 4 MB of partial sums: the allocator keeps it until the fold ran
-    sink.ready()  # the bucket's work is issued from the dW stream, after the fold
+    """dx of the (add-)norm backward; dW folded into ``sink`` (then ``sink.ready()``).
+    (Folding dW on the dW side stream instead was measured at no gain:
+    profiles/r1_norm_fold_side_ab.log.)"""
+    dx = kernels().norm_bwd(dy, x, w, rstd, mean, sink.buf, dres, sink.accumulate)
+    sink.ready()
     return dx
 
 
@@ -209,6 +192,13 @@ class EmbeddingFn(torch.autograd.Function):
         sink = ctx.sink
         dy = dy.contiguous()
         if sink is not None and sink.gather is not None:
+            if sink.defer:  # accumulation micro-batch: exchanged with the last one
+                sink.stash.append((tokens.reshape(-1), dy.reshape(-1, dy.shape[-1])))
+                return None, None, None
+            if sink.stash:
+                tokens = torch.cat([t for t, _ in sink.stash] + [tokens.reshape(-1)])
+                dy = torch.cat([g for _, g in sink.stash] + [dy.reshape(-1, dy.shape[-1])])
+                sink.stash = []
             # DP sparse exchange: every rank's (token, dY) rows, scatter-added locally
             tokens, dy = sink.gather(tokens, dy)
         if dy.is_cuda:

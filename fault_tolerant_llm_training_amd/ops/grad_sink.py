@@ -15,7 +15,7 @@ import torch
 
 
 class GradSink:
-    __slots__ = ("buf", "start", "end", "accumulate", "hook", "name", "gather")
+    __slots__ = ("buf", "start", "end", "accumulate", "hook", "name", "gather", "defer", "stash")
 
     def __init__(self, buf: torch.Tensor, start: int = 0, end: int = 0, name: str = ""):
         self.buf = buf
@@ -26,6 +26,10 @@ class GradSink:
         self.name = name
         # data parallel: (tokens, dy) -> every rank's (tokens, dy) (sparse embedding exchange)
         self.gather: Optional[Callable] = None
+        # gradient accumulation with the sparse exchange: rows of non-final micro-batches are
+        # stashed here (defer=True) and exchanged together in the last micro-batch
+        self.defer = False
+        self.stash: list = []
 
     def ready(self) -> None:
         if self.hook is not None:

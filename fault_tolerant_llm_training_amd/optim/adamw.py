@@ -22,8 +22,15 @@ GPU step (with a :class:`~..parallel.ddp.GradReducer`):
    overlaps the compute-bound GEMMs of the next step instead of running as a
    serial phase.
 
-A non-finite norm makes every update kernel skip (no host sync);
-:meth:`check_finite` reports it one step later.
+A non-finite norm makes every update kernel skip (no host sync), and the flag is
+*sticky*: every later step skips too until :meth:`reset_nonfinite`. The host
+reads each step's ``[norm, coef, nonfinite]`` from a small ring of pinned
+copies; the trainer checks step ``k`` at the boundary before step ``k+2``
+(that copy has long landed, so the check never stalls the pipeline) and, on a
+bad step, rolls the host counters back to it with :meth:`rollback_steps`:
+parameters and moments are still exactly those before the bad step, which is
+what the reference's ``error_if_nonfinite`` raise before ``optimizer.step()``
+leaves behind (reference utils.py:61, train.py:107-109).
 """
 from __future__ import annotations
 
@@ -80,6 +87,8 @@ class ParamGate:
 
 
 class FlatAdamW(torch.optim.Optimizer):
+    RING = 4  # pinned stats copies kept (the trainer checks two steps late)
+
     def __init__(self, params, flat: FlatParamSpace, lr: float = 1e-3, betas=(0.9, 0.999),
                  eps: float = 1e-8, weight_decay: float = 1e-2, state_dtype: Optional[torch.dtype] = None,
                  max_grad_norm: float = 0.0, fused: bool = True, reducer=None):
@@ -98,7 +107,12 @@ class FlatAdamW(torch.optim.Optimizer):
         self.step_count = 0
         self.max_grad_norm = float(max_grad_norm)
         self.stats = torch.zeros(3, dtype=torch.float32, device=flat.device)  # norm, coef, nonfinite
-        self._host_stats = torch.zeros(3, dtype=torch.float32, pin_memory=flat.device.type == "cuda")
+        # ring of per-step host copies: step -> (pinned [3] copy, event or None)
+        self._pin = flat.device.type == "cuda"
+        self._ring = [torch.zeros(3, dtype=torch.float32, pin_memory=self._pin) for _ in range(self.RING)]
+        self._ring_events = [None] * self.RING
+        self._ring_steps = [-1] * self.RING
+        self._checked_step = 0  # every step <= this one is known finite
         self._stats_event = None
         self._stats_step = -1
         self.gate = ParamGate()
@@ -169,7 +183,9 @@ class FlatAdamW(torch.optim.Optimizer):
                 self._update(r.param_for_update(b), r.grad_for_update(b), self.exp_avg[slo:shi],
                              self.exp_avg_sq[slo:shi], lr, b1, b2, eps, wd,
                              self.overlap_blocks if r.overlap else 0)
-                if self.zero1:
+                if self.zero1 and r.dry_comm:
+                    pass
+                elif self.zero1:
                     work = dist.all_gather_into_tensor(f.params[b.lo : b.hi], r.param_shard(b),
                                                        group=r.group, async_op=True)
                     if r.overlap:
@@ -182,41 +198,93 @@ class FlatAdamW(torch.optim.Optimizer):
         return None
 
     def _publish_stats(self):
+        i = self.step_count % self.RING
+        h = self._ring[i]
         if self.stats.is_cuda:
-            self._host_stats.copy_(self.stats, non_blocking=True)
-            if self._stats_event is None:
-                self._stats_event = torch.cuda.Event()
-            self._stats_event.record()
+            h.copy_(self.stats, non_blocking=True)
+            ev = self._ring_events[i]
+            if ev is None:
+                ev = self._ring_events[i] = torch.cuda.Event()
+            ev.record()
+            self._stats_event = ev
         else:
-            self._host_stats.copy_(self.stats)
+            h.copy_(self.stats)
+        self._ring_steps[i] = self.step_count
         self._stats_step = self.step_count
 
     def norm_for_logging(self):
         """(device tensor holding the last step's pre-clip grad norm, event after which it is valid)."""
         return self.stats[:1], self._stats_event
 
-    def check_finite(self, block: bool = False) -> Optional[float]:
-        """Deferred non-finite check of the last step's gradient norm.
+    def _step_stats(self, step: int, block: bool):
+        """Host copy [norm, coef, nonfinite] of optimizer step ``step`` (None if not ready / gone)."""
+        i = step % self.RING
+        if self._ring_steps[i] != step:
+            return None
+        ev = self._ring_events[i]
+        if ev is not None:
+            if block:
+                ev.synchronize()
+            elif not ev.query():
+                return None
+        return self._ring[i].tolist()
 
-        Returns the norm when available. Raises :class:`NonFiniteGradError` (the
-        reference's ``error_if_nonfinite`` RuntimeError path) if it was not finite.
+    def first_nonfinite(self, upto: Optional[int] = None, block: bool = True) -> Optional[int]:
+        """Oldest optimizer step in ``(checked, upto]`` whose gradient norm was not finite.
+
+        ``upto`` defaults to the last step taken. The flag is sticky, so step ``upto``
+        alone tells whether any step before it was bad; only then is the ring scanned for
+        the first bad one (where the state stopped changing). Steps found finite are never
+        read again. A non-blocking call returns None while step ``upto``'s copy is in flight."""
+        upto = self.step_count if upto is None else min(int(upto), self.step_count)
+        if upto <= self._checked_step:
+            return None
+        st = self._step_stats(upto, block)
+        if st is None:
+            return None
+        if not st[2]:
+            self._checked_step = upto
+            return None
+        for k in range(max(self._checked_step + 1, self.step_count - self.RING + 1), upto):
+            sk = self._step_stats(k, True)
+            if sk is not None and sk[2]:
+                return k
+        return upto
+
+    def last_norm(self) -> Optional[float]:
+        st = self._step_stats(self.step_count, True) if self.step_count > 0 else None
+        return None if st is None else st[0]
+
+    def check_finite(self, block: bool = False) -> Optional[float]:
+        """Non-finite check of every step so far (stand-alone use: bench, smoke, tests).
+
+        Returns the last step's norm when available. Raises :class:`NonFiniteGradError` (the
+        reference's ``error_if_nonfinite`` RuntimeError path) if some step was not finite.
         """
-        if self._stats_step < 0:
+        if self.step_count == 0:
             return None
-        ev = self._stats_event
-        if ev is not None and not block and not ev.query():
-            return None
-        if ev is not None and block:
-            ev.synchronize()
-        norm, _coef, bad = self._host_stats.tolist()
-        if bad:
-            step = self._stats_step
-            self._stats_step = -1
-            raise NonFiniteGradError(
-                f"The total norm of order 2.0 for gradients from `parameters` is non-finite at optimizer step {step}, "
-                "so it cannot be clipped (update skipped)."
-            )
-        return norm
+        bad = self.first_nonfinite(block=block)
+        if bad is not None:
+            raise NonFiniteGradError(nonfinite_message(bad))
+        st = self._step_stats(self.step_count, block)
+        return None if st is None else st[0]
+
+    @torch.no_grad()
+    def reset_nonfinite(self) -> None:
+        """Clear the sticky skip flag (after the state was restored from a checkpoint)."""
+        self.stats.zero_()
+        self._checked_step = self.step_count
+
+    def rollback_steps(self, k: int) -> None:
+        """Undo the host-side bookkeeping of the last ``k`` optimizer steps, whose updates the
+        (sticky) non-finite guard skipped on device: step counter and stats ring only."""
+        if k <= 0:
+            return
+        self.step_count -= k
+        self._checked_step = min(self._checked_step, self.step_count)
+        for i in range(self.RING):
+            if self._ring_steps[i] > self.step_count:
+                self._ring_steps[i] = -1
 
     def zero_grad(self, set_to_none: bool = True):
         """No-op: every backward overwrites the flat gradient buffer (beta=0 writes)."""
@@ -300,11 +368,17 @@ class FlatAdamW(torch.optim.Optimizer):
         return self.exp_avg, self.exp_avg_sq
 
 
+def nonfinite_message(step: int) -> str:
+    return (f"The total norm of order 2.0 for gradients from `parameters` is non-finite at optimizer step {step}, "
+            "so it cannot be clipped (update skipped).")
+
+
 def _norm_reference(sumsq: torch.Tensor, stats: torch.Tensor, max_norm: float) -> None:
     norm = float(sumsq.sqrt())
     bad = not math.isfinite(norm)
     coef = 1.0 if (max_norm <= 0 or bad) else min(1.0, max_norm / (norm + 1e-6))
-    stats.copy_(torch.tensor([norm, coef, 1.0 if bad else 0.0]))
+    sticky = bad or float(stats[2]) != 0.0  # same sticky flag as norm_finish_kernel
+    stats.copy_(torch.tensor([norm, coef, 1.0 if sticky else 0.0]))
 
 
 def _adamw_reference(p, g, m, v, stats, lr, b1, b2, eps, wd, step):

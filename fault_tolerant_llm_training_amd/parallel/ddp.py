@@ -16,6 +16,16 @@ work is launched while the compute stream keeps running backward:
                         shard, an ``all_gather`` republishes the bucket's
                         parameters (``optim.adamw``).
 
+Buckets launch strictly in index order (a bucket that completes early waits for
+the ones above it), so every rank issues the same collective sequence; that is
+what lets a rank whose step failed half-way (:meth:`GradReducer.poison_and_complete`)
+issue exactly the collectives its peers are waiting for.
+
+Gradient accumulation (``--grad-accum K``): micro-batches ``0..K-2`` only
+accumulate into the flat buffer (sinks in accumulate mode, no collectives,
+embedding rows stashed); the buckets launch during the last micro-batch's
+backward, so the collective volume per optimizer step is independent of K.
+
 So the gradient norm needed for clipping (reference utils.py:58-63) is
 finished a few µs after backward ends, and the optimizer (which the
 reference runs as a separate serial phase, train.py:107-109) starts at once.
@@ -168,10 +178,19 @@ class GradReducer:
         if self.cuda:
             for b in self.buckets:
                 b.event = torch.cuda.Event()
+        self._extra_sinks = list(extra_sinks)
         for sink in list(flat.sinks.values()) + list(extra_sinks):
             sink.hook = self._on_ready
         self.comm = self.world > 1 or mode != "local"
         self._pending_sumsq: List[Bucket] = []
+        self._next = 0            # index of the next bucket to launch (in-order launch)
+        self.fault_after_buckets = 0  # fault-injection hook: raise after this many launches
+        # benchmark only (bench.py exposed-communication estimate): skip every collective so a
+        # rank runs the same kernels without waiting on peers; gradients are then rank-local
+        self.dry_comm = False
+        self.sync = True          # False during the non-final micro-batches of an accumulation
+        self.gathered = False     # the sparse embedding exchange of this step has run
+        self.emb_sink = flat.sinks.get(emb) if self.sparse_embedding else None
 
     # ---------------------------------------------------------------- shard views
     def param_shard(self, b: Bucket) -> torch.Tensor:
@@ -188,8 +207,11 @@ class GradReducer:
 
     def _gather_rows(self, tokens: torch.Tensor, dy: torch.Tensor):
         """All-gather every rank's (tokens [T], dY [T, D]) — rank order, deterministic."""
+        self.gathered = True
         t = tokens.reshape(-1).contiguous()
         d = dy.reshape(t.numel(), -1).contiguous()
+        if self.dry_comm:
+            return t, d
         t_all = torch.empty(self.world * t.numel(), dtype=t.dtype, device=t.device)
         d_all = torch.empty(self.world * d.shape[0], d.shape[1], dtype=d.dtype, device=d.device)
         dist.all_gather_into_tensor(t_all, t, group=self.group)
@@ -206,15 +228,40 @@ class GradReducer:
         return b.lo, b.hi
 
     # ---------------------------------------------------------------- backward hooks
+    def begin_micro(self, k: int, n: int) -> None:
+        """Micro-batch ``k`` of ``n`` (gradient accumulation) is about to run forward/backward."""
+        last = k == n - 1
+        self.sync = last
+        for sink in self.flat.sinks.values():
+            sink.accumulate = k > 0
+        for sink in self._extra_sinks:
+            sink.accumulate = k > 0
+        if self.emb_sink is not None:
+            # the sparse exchange sums every rank's rows of every micro-batch at once (in the
+            # last backward), so the dense embedding gradient is written once, not accumulated
+            self.emb_sink.accumulate = False
+            self.emb_sink.defer = not last
+            if k == 0:
+                self.emb_sink.stash = []
+
     def _on_ready(self, sink: GradSink) -> None:
-        for b in self.buckets:
+        if not self.sync:
+            return  # accumulation micro-batch: no collectives, no sums yet
+        for b in self.buckets[self._next:]:
             if b.hi <= sink.start:
                 break  # buckets are in descending address order
             ov = min(b.hi, sink.end) - max(b.lo, sink.start)
             if ov > 0:
                 b.filled += ov
-                if b.filled >= b.needed and not b.launched:
-                    self._launch(b)
+        while self._next < len(self.buckets):
+            b = self.buckets[self._next]
+            if b.filled < b.needed:
+                break
+            self._next += 1
+            self._launch(b)
+            if self.fault_after_buckets and self._next >= self.fault_after_buckets:
+                self.fault_after_buckets = 0  # test hook (trainer FT_INJECT_FAULT=r:s:backward)
+                raise OSError(5, "injected I/O error inside backward (after a bucket launch)")
 
     def _sumsq(self, g: torch.Tensor, b: Bucket) -> None:
         part = self.partials[b.part_lo : b.part_hi]
@@ -241,8 +288,8 @@ class GradReducer:
     def _launch_now(self, b: Bucket) -> None:
         b.launched = True
         grads = self.flat.grads[b.lo : b.hi]
-        if b.sparse:
-            pass  # summed by the sparse embedding exchange inside the embedding backward
+        if b.sparse or self.dry_comm:
+            pass  # sparse: summed by the embedding exchange inside the embedding backward
         elif self.mode == "allreduce":
             b.work = dist.all_reduce(grads, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
         elif self.mode == "zero1":
@@ -271,9 +318,10 @@ class GradReducer:
             from ..ops.functional import join_dw_stream
 
             join_dw_stream()  # weight gradients still running on the dW side stream
-        for b in self.buckets:
-            if not b.launched:
-                self._launch(b)
+        while self._next < len(self.buckets):
+            b = self.buckets[self._next]
+            self._next += 1
+            self._launch(b)
         if self._pending_sumsq:  # A/B mode: all partial sums after backward, one pass
             with torch.cuda.stream(self.side):
                 for b in self._pending_sumsq:
@@ -288,6 +336,47 @@ class GradReducer:
         for b in self.buckets:
             b.filled = 0
             b.launched = False
+        self._next = 0
+        self.gathered = False
+
+    @torch.no_grad()
+    def poison_and_complete(self, tokens_shape=None, dim: int = 0) -> None:
+        """Finish this rank's share of the step's collectives after a local failure.
+
+        Peers that are still inside the step wait for this rank's remaining bucket
+        collectives (and the sparse embedding exchange). Every bucket not yet launched is
+        filled with NaN and launched in the usual order, so the peers' collectives complete
+        and the reduced gradient — hence the global norm — is NaN on every rank: the
+        non-finite guard then skips this step's update everywhere and all ranks keep the
+        parameters/moments of the previous step (see ``FlatAdamW.first_nonfinite``).
+        Afterwards the caller runs ``optimizer.step()`` as usual (ZeRO-1's norm all-reduce
+        and parameter all-gathers are collectives too)."""
+        self.sync = True
+        nan = float("nan")
+        poisoned = False
+        for b in self.buckets[self._next:]:
+            self.flat.grads[b.lo : b.hi].fill_(nan)
+            poisoned = True
+        # the peers' order: every dense bucket (they all complete before the embedding
+        # backward), then the sparse embedding exchange, then the embedding bucket
+        while self._next < len(self.buckets) and not self.buckets[self._next].sparse:
+            b = self.buckets[self._next]
+            self._next += 1
+            self._launch(b)
+        if self.sparse_embedding and not self.gathered:
+            T = 1
+            for s_ in tokens_shape or (1,):
+                T *= int(s_)
+            tok = torch.zeros(T, dtype=torch.long, device=self.flat.device)
+            dy = torch.full((T, dim), nan, dtype=self.flat.dtype, device=self.flat.device)
+            self._gather_rows(tok, dy)
+            es = self.emb_sink
+            self.flat.grads[es.start : es.end].fill_(nan)
+            poisoned = True
+        # (nothing poisoned: every collective already went out with valid data, so the
+        # peers' step — and this rank's, once the caller runs the optimizer — is valid)
+        del poisoned
+        self.finish()
 
     def global_sumsq(self) -> torch.Tensor:
         """Partials reduced across ranks when each rank only holds a shard (ZeRO-1).
@@ -299,7 +388,8 @@ class GradReducer:
             torch.sum(self.partials, dim=0, keepdim=True, out=self.sumsq_total)
         else:
             self.sumsq_total.copy_(self.partials.sum().reshape(1))
-        dist.all_reduce(self.sumsq_total, op=dist.ReduceOp.SUM, group=self.group)
+        if not self.dry_comm:
+            dist.all_reduce(self.sumsq_total, op=dist.ReduceOp.SUM, group=self.group)
         return self.sumsq_total
 
     @torch.no_grad()
@@ -313,6 +403,3 @@ class GradReducer:
         return (f"{self.mode}: {len(self.buckets)} buckets, {min(sizes):.0f}-{max(sizes):.0f} MiB"
                 + (f", shard {self.shard_numel * es / 2**30:.2f} GiB/rank" if self.mode == "zero1" else ""))
 
-
-# Back-compat name used by early scripts.
-FlatDDP = GradReducer

@@ -8,7 +8,13 @@ or Slurm (SLURM_PROCID/SLURM_LOCALID/SLURM_NTASKS). Two groups are created:
   gradient all-reduce — stream-ordered, never blocks the host;
 * a ``gloo`` CPU group for control-plane agreement (stop-signal consensus,
   token counts, data-loader states, config checks), so a 4-byte vote never
-  forces a GPU synchronisation.
+  forces a GPU synchronisation;
+* a second ``gloo`` group with a SHORT timeout (``--peer-timeout``, default
+  60 s) used only by the per-step vote: a peer that died (SIGKILL, OOM kill)
+  closes its sockets and fails the vote at once; one that hangs fails it after
+  the timeout. Either way the survivors learn it well inside Slurm's 120 s
+  ``USR1`` lead instead of the 30-minute default collective timeout, and
+  :class:`PeerFailure` is raised.
 """
 from __future__ import annotations
 
@@ -29,6 +35,8 @@ class DistInfo:
     device: torch.device = torch.device("cpu")
     ctrl_group: Optional[object] = None  # gloo group (None when world_size == 1)
     ckpt_group: Optional[object] = None  # gloo group used only by checkpoint writer threads
+    vote_group: Optional[object] = None  # gloo group with the short peer timeout (per-step vote)
+    peer_timeout_s: float = 60.0
 
     @property
     def is_main(self) -> bool:
@@ -42,6 +50,10 @@ class DistInfo:
 _INFO: Optional[DistInfo] = None
 
 
+class PeerFailure(RuntimeError):
+    """A peer rank stopped answering the control plane (died, or hung past the peer timeout)."""
+
+
 def env_ranks():
     env = os.environ
     if "RANK" in env and "WORLD_SIZE" in env:
@@ -51,7 +63,7 @@ def env_ranks():
     return 0, 1, int(env.get("LOCAL_RANK", 0))
 
 
-def init_distributed(device_type: str = "cuda", timeout_s: int = 1800) -> DistInfo:
+def init_distributed(device_type: str = "cuda", timeout_s: int = 1800, peer_timeout_s: float = 60.0) -> DistInfo:
     global _INFO
     if _INFO is not None:
         return _INFO
@@ -61,7 +73,7 @@ def init_distributed(device_type: str = "cuda", timeout_s: int = 1800) -> DistIn
         device = torch.device("cuda", local)
     else:
         device = torch.device("cpu")
-    info = DistInfo(rank, world, local, device)
+    info = DistInfo(rank, world, local, device, peer_timeout_s=float(peer_timeout_s))
     # FT_FORCE_DIST=1 builds the process groups even for one rank (exercises the RCCL path on 1 GPU)
     if world > 1 or os.environ.get("FT_FORCE_DIST") == "1":
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -80,6 +92,7 @@ def init_distributed(device_type: str = "cuda", timeout_s: int = 1800) -> DistIn
         # a second gloo group so background checkpoint-writer threads never interleave
         # their collectives with the main thread's control-plane votes
         info.ckpt_group = dist.new_group(backend="gloo", timeout=timeout)
+        info.vote_group = dist.new_group(backend="gloo", timeout=datetime.timedelta(seconds=peer_timeout_s))
     _INFO = info
     return info
 
@@ -123,6 +136,25 @@ def ctrl_broadcast_object(obj, src: int = 0):
     box = [obj]
     dist.broadcast_object_list(box, src=src, group=info.ctrl_group)
     return box[0]
+
+
+def vote(values):
+    """All-gather a short float vector from every rank over the short-timeout gloo group.
+
+    Returns a [world, len(values)] float64 tensor (row r = rank r's values); every rank
+    gets the same table, so MAX/SUM/first-rank decisions taken from it agree. Any
+    failure of the exchange (peer gone or hung past ``--peer-timeout``) raises
+    :class:`PeerFailure`."""
+    info = get_info()
+    t = torch.tensor([float(v) for v in values], dtype=torch.float64)
+    if not info.distributed:
+        return t.view(1, -1)
+    out = torch.empty(info.world_size * t.numel(), dtype=torch.float64)
+    try:
+        dist.all_gather_into_tensor(out, t, group=info.vote_group)
+    except Exception as e:  # noqa: BLE001 - gloo raises RuntimeError/DistBackendError subclasses
+        raise PeerFailure(f"step vote failed (peer rank lost or hung > {info.peer_timeout_s:.0f}s): {e}") from e
+    return out.view(info.world_size, -1)
 
 
 def barrier():

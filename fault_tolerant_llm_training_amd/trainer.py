@@ -26,8 +26,10 @@ HIP kernels, bucketed RCCL all-reduce overlapped with backward
 """
 from __future__ import annotations
 
+import collections
 import json
 import os
+import signal
 import sys
 import time
 from typing import Any, Dict, Optional
@@ -42,13 +44,14 @@ from .data.synthetic import SyntheticTokens
 from .ft.exit_handler import classify_exception, handle_exit
 from .ft.signals import SignalInterrupt, SignalMonitor
 from .models.llama import build_model, flops_per_token, model_args_for
-from .optim.adamw import FlatAdamW
+from .optim.adamw import FlatAdamW, NonFiniteGradError, nonfinite_message
 from .parallel import dist as fdist
 from .parallel.ddp import GradReducer
 from .utils.config import PRECISION_STR_TO_DTYPE, get_args, jobid
 from .utils.logging import init_logger, logger
-from .utils.lr import build_lr_scheduler
+from .utils.lr import build_lr_scheduler, rollback_lr_scheduler
 
+SIGTERM_NUM = int(signal.SIGTERM)
 SYNTHETIC_VOCAB = 131072  # the reference's Mistral-Nemo tokenizer size
 
 
@@ -60,26 +63,25 @@ class InjectedFault(Exception):
 
 
 class _LossLog:
-    """Deferred step logging without host stalls.
+    """Step logging without host stalls, summed over data-parallel ranks.
 
-    At a log step the loss is copied D2H into pinned memory and a timing event is
-    recorded on the compute stream; the line is printed at a later step boundary
-    once the event has completed. Step time is the GPU time between consecutive
-    log events (the host runs ahead of the GPU, so host timestamps would measure
-    enqueue time, not step time).
+    At a log step the loss (and grad norm) is copied D2H into pinned memory behind
+    an event on the compute stream. Two step boundaries later — when that copy has
+    long landed — :meth:`take` hands the entry to the trainer, which adds the local
+    value to the per-step vote; the vote returns the ranks' sum (each rank's loss
+    is its token sum over the GLOBAL token count, so the sum is the global-batch
+    mean) and :meth:`emit` prints the reference's line. No data-plane collective and
+    no device sync is needed for logging. Step time is the GPU time between
+    consecutive log events (the host runs ahead of the GPU).
     """
 
     def __init__(self, device: torch.device, tokens_per_step: int, world: int, flops_per_token: float):
         self.cuda = device.type == "cuda"
-        self.pending = []  # (step, host loss, event, extra)
+        self.pending = []  # [step, host values, event or host time, extra]
         self.tokens = tokens_per_step
         self.world = world
         self.fpt = flops_per_token
         self.last = None  # (step, event or host time)
-
-    def mark(self):
-        """Timing origin (call once the first step is enqueued)."""
-        self.last = None
 
     def push(self, step: int, loss: torch.Tensor, extra: Dict[str, Any], norm=None):
         """``norm``: optional (device tensor, event) of the step's gradient norm (logged as grad_norm)."""
@@ -93,42 +95,89 @@ class _LossLog:
             h.copy_(torch.cat(vals), non_blocking=True)
             ev = torch.cuda.Event(enable_timing=True)
             ev.record()
-            self.pending.append((step, h, ev, extra))
+            self.pending.append([step, h, ev, extra])
         else:
-            self.pending.append((step, torch.cat(vals), time.perf_counter(), extra))
+            self.pending.append([step, torch.cat(vals), time.perf_counter(), extra])
 
-    def flush(self, force: bool = False):
-        keep = []
-        for step, h, ev, extra in self.pending:
-            if self.cuda and not force and not ev.query():
-                keep.append((step, h, ev, extra))
-                continue
+    def take(self, upto: int):
+        """Entries of steps <= ``upto`` (host values ready; blocks on their copies)."""
+        out = [e for e in self.pending if e[0] <= upto]
+        self.pending = [e for e in self.pending if e[0] > upto]
+        for e in out:
             if self.cuda:
-                ev.synchronize()
-            hv = h.tolist()
-            msg = f"Training step: {step} | Loss: {hv[0]:.2f}"
-            if len(hv) > 1:
-                extra = dict(extra)
-                extra["grad_norm"] = f"{hv[1]:.3f}"
-            if self.last is not None:
-                ls, lev = self.last
-                dt = (lev.elapsed_time(ev) / 1e3) if self.cuda else (ev - lev)
-                dt /= max(1, step - ls)
-                tok_s = self.tokens / dt
-                extra = dict(extra)
-                extra["step_ms"] = f"{dt * 1e3:.1f}"
-                extra["tok/s"] = f"{tok_s:.0f}"
-                if self.cuda:
-                    extra["MFU"] = f"{tok_s / self.world * self.fpt / 2.5e15:.3f}"
-            self.last = (step, ev)
-            if extra:
-                msg += " | " + " | ".join(f"{k}: {v}" for k, v in extra.items())
-            logger.info(msg)
-        self.pending = keep
+                e[2].synchronize()
+            e[1] = e[1].tolist()
+        return out
+
+    def emit(self, e, loss: float) -> None:
+        step, hv, ev, extra = e
+        msg = f"Training step: {step} | Loss: {loss:.2f}"
+        extra = dict(extra)
+        if len(hv) > 1:
+            extra["grad_norm"] = f"{hv[1]:.3f}"
+        if self.last is not None and step > self.last[0]:
+            ls, lev = self.last
+            dt = (lev.elapsed_time(ev) / 1e3) if self.cuda else (ev - lev)
+            dt /= max(1, step - ls)
+            tok_s = self.tokens / dt
+            extra["step_ms"] = f"{dt * 1e3:.1f}"
+            extra["tok/s"] = f"{tok_s:.0f}"
+            if self.cuda:
+                extra["MFU"] = f"{tok_s / self.world * self.fpt / 2.5e15:.3f}"
+        self.last = (step, ev)
+        if extra:
+            msg += " | " + " | ".join(f"{k}: {v}" for k, v in extra.items())
+        logger.info(msg)
+
+    def drop_after(self, step: int) -> None:
+        """Forget entries of rolled-back steps."""
+        self.pending = [e for e in self.pending if e[0] < step]
+
+
+class _StopTraining(Exception):
+    """Raised at a step boundary once every rank has agreed to stop (carries the exit cause)."""
+
+    def __init__(self, cause: BaseException):
+        super().__init__(repr(cause))
+        self.cause = cause
+
+
+class _FatalStepError(Exception):
+    """A failure left this rank unable to finish its share of the step's collectives."""
+
+
+class _RankFault:
+    """Rank-local fault injection for the DP tests: ``FT_INJECT_FAULT=rank:step:phase``.
+
+    Phases: ``data`` (OSError while fetching the batch), ``forward``, ``backward`` (OSError
+    raised inside backward after the first gradient bucket was launched), ``optimizer``
+    (before ``optimizer.step()``), ``post`` (after the step), ``kill`` (SIGKILL itself) and
+    ``hang`` (sleep forever) at the start of the step."""
+
+    def __init__(self, spec: str, rank: int):
+        self.step = self.phase = None
+        if spec:
+            r, st, ph = spec.split(":")
+            if int(r) == rank:
+                self.step, self.phase = int(st), ph
+
+    def at(self, step: int, phase: str) -> bool:
+        return self.step == step and self.phase == phase
+
+    def fire(self, step: int, phase: str) -> None:
+        if not self.at(step, phase):
+            return
+        if phase == "kill":
+            os.kill(os.getpid(), signal.SIGKILL)
+        if phase == "hang":
+            while True:
+                time.sleep(1)
+        raise OSError(5, f"injected I/O error on this rank at step {step} ({phase})")
 
 
 def _build_source(args, info, tokenizer_vocab_holder: Dict[str, Any]):
-    B, S = args.batch_size, args.sequence_length
+    # one loader batch = the K micro-batches of one optimizer step (gradient accumulation)
+    B, S = args.batch_size * max(1, int(args.grad_accum)), args.sequence_length
     if args.synthetic_data:
         vocab = args.vocab_size or SYNTHETIC_VOCAB
         tokenizer_vocab_holder["vocab"] = vocab
@@ -150,7 +199,7 @@ def _build_source(args, info, tokenizer_vocab_holder: Dict[str, Any]):
 
 def train(args) -> int:
     t_setup = time.perf_counter()
-    info = fdist.init_distributed(args.device)
+    info = fdist.init_distributed(args.device, peer_timeout_s=args.peer_timeout)
     init_logger(info.rank)
     logger.info(f"Experiment args: {args}")
     # Install the flag handlers before any slow setup: a signal that arrives while
@@ -272,14 +321,13 @@ def train(args) -> int:
         # SIGUSR1 one, racing the Slurm deadline) then only copies and writes
         ckpt_engine().preallocate_async()
 
-    def save_checkpoint(blocking: bool, collective: bool = True):
+    # loader position before each step (what a checkpoint taken at that step boundary records)
+    loader_at: Dict[int, Any] = {}
+
+    def save_checkpoint(blocking: bool, step_now: int):
+        """Collective save of the state at step boundary ``step_now`` (every rank calls it)."""
         optimizer.gate.wait_all()  # the snapshot must follow this step's parameter updates
-        if collective:
-            states = fdist.ctrl_all_gather_object(loader.state_dict())
-        else:  # rank-local save (error on this rank only): other ranks' positions unknown
-            states = [None] * info.world_size
-            states[info.rank] = loader.state_dict()
-        step_now = training_step
+        states = fdist.ctrl_all_gather_object(loader_at.get(step_now, loader.state_dict()))
         rng = capture_rng(device)
 
         def build(host):
@@ -287,79 +335,196 @@ def train(args) -> int:
                                     data_loader=states if info.distributed else states[0], rng=rng,
                                     extra_meta={"world_size": info.world_size, "job_id": str(job_id)})
 
-        if sharded and not collective:
-            if optimizer.zero1:
-                logger.error("ZeRO-1 optimizer state is sharded over the ranks; a rank-local error cannot "
-                             "write a complete checkpoint")
-                return False
-            # replicated state: this rank writes the whole file alone
-            solo = CheckpointEngine({"params": model.flat.params, "exp_avg": optimizer.exp_avg,
-                                     "exp_avg_sq": optimizer.exp_avg_sq}, mode="host",
-                                    writer_threads=args.checkpoint_writer_threads)
-            return solo.save(ckpt_path, build, step=step_now, blocking=True)
         engine = ckpt_engine()
         writes = sharded or info.is_main
         st = engine.save(ckpt_path, build, step=step_now, blocking=blocking) if writes else None
-        if collective and blocking:
+        if blocking:
             fdist.barrier()
         return st
 
+    def save_solo(step_now: int):
+        """Peer lost: one surviving rank writes the whole (replicated) state alone. Returns
+        False when this rank cannot (sharded optimizer state, incomplete state, another
+        survivor already writing)."""
+        if optimizer.zero1 or source.kind == "iterable":
+            logger.error("[EXIT HANDLER] optimizer or data-loader state is sharded over the ranks; "
+                         "no complete checkpoint can be written without the lost peer")
+            return False
+        os.makedirs(os.path.dirname(ckpt_path) or ".", exist_ok=True)
+        try:  # first survivor wins; the others leave the file to it
+            os.close(os.open(ckpt_path + ".solo", os.O_CREAT | os.O_EXCL | os.O_WRONLY, 0o644))
+        except FileExistsError:
+            logger.info("[EXIT HANDLER] another surviving rank is writing the checkpoint")
+            return None
+        me = loader_at.get(step_now, loader.state_dict())
+        states = [dict(me) for _ in range(info.world_size)]  # stateless sources: same next_step everywhere
+        rng = capture_rng(device)
+
+        def build(host):
+            return build_checkpoint(model, optimizer, lr_scheduler, step_now, host,
+                                    data_loader=states if info.distributed else states[0], rng=rng,
+                                    extra_meta={"world_size": info.world_size, "job_id": str(job_id)})
+
+        solo = CheckpointEngine({"params": model.flat.params, "exp_avg": optimizer.exp_avg,
+                                 "exp_avg_sq": optimizer.exp_avg_sq}, mode="host",
+                                writer_threads=args.checkpoint_writer_threads)
+        # (the lock file stays: a slower survivor must not write the file a second time)
+        return solo.save(ckpt_path, build, step=step_now, blocking=True)
+
     metrics_f = open(args.metrics_file, "a") if (args.metrics_file and info.is_main) else None
     B, S, W = args.batch_size, args.sequence_length, info.world_size
+    K = max(1, int(args.grad_accum))
     fpt = flops_per_token(margs, S)
-    losslog = _LossLog(device, B * S * W, W, fpt)
+    losslog = _LossLog(device, B * K * S * W, W, fpt)
     synthetic_counts = args.synthetic_data  # no ignore_index labels: the global count is static
     inv_static = None
     if synthetic_counts:
-        inv_static = torch.full((1,), 1.0 / (B * S * W), dtype=torch.float32, device=device)
+        inv_static = torch.full((1,), 1.0 / (B * K * S * W), dtype=torch.float32, device=device)
     t_window, steps_window = time.perf_counter(), 0
     logger.info(f"Setup took {time.perf_counter() - t_setup:.2f}s")
     prof, prof_range = None, None
     if args.profile_steps:
         a0, a1 = (int(v) for v in args.profile_steps.split(":"))
         prof_range = (a0, a1)
+    fault = _RankFault(os.environ.get("FT_INJECT_FAULT", ""), info.rank)
+    # optimizer step k <-> training step k - offset (0 for fresh runs; resumed runs load both)
+    offset = optimizer.step_count - training_step
+    pending_err: Optional[BaseException] = None  # this rank's mid-step failure (step completed poisoned)
+
+    def rollback_to_first_bad() -> Optional[int]:
+        """Blocking check of every optimizer step so far; roll host counters back to the first
+        non-finite one (its update and every later one were skipped on device)."""
+        nonlocal training_step
+        bad = optimizer.first_nonfinite(block=True)
+        if bad is None:
+            return None
+        k = optimizer.step_count - bad + 1
+        optimizer.rollback_steps(k)
+        rollback_lr_scheduler(lr_scheduler, k)
+        training_step -= k
+        losslog.drop_after(training_step)
+        return training_step
+
+    def boundary(final: bool = False) -> None:
+        """Step boundary: one vote over every rank (signal, local error, lagged non-finite check,
+        token count of the next batch, losses to log), then either go on or stop together."""
+        nonlocal pending_err
+        sig = monitor.pending()
+        err = 1.0 if pending_err is not None else 0.0
+        upto = optimizer.step_count if final else optimizer.step_count - 1
+        bad = optimizer.first_nonfinite(upto=upto, block=True)
+        entries = losslog.take(training_step - (0 if final else 2))
+        vec = [float(sig), err, float(bad or 0), float(boundary.count)] + [e[1][0] for e in entries]
+        table = fdist.vote(vec)
+        for e, lv in zip(entries, table[:, 4:].sum(0).tolist()):
+            losslog.emit(e, lv)
+        boundary.count_sum = float(table[:, 3].sum())
+        sig_all = int(table[:, 0].max())
+        err_all = bool(table[:, 1].max() > 0)
+        bad_all = bool(table[:, 2].max() > 0)
+        if not (sig_all or err_all or bad_all):
+            return
+        # stop: every rank reached the same decision from the same table
+        rolled = rollback_to_first_bad()
+        if sig_all == SIGTERM_NUM:
+            raise _StopTraining(SignalInterrupt(sig_all))
+        if pending_err is not None:
+            raise _StopTraining(pending_err)
+        if err_all:
+            raise _StopTraining(RuntimeError("a peer rank failed during training (see its log); "
+                                             "stopping every rank at the same step"))
+        if rolled is not None:
+            raise _StopTraining(NonFiniteGradError(nonfinite_message(rolled + offset + 1)))
+        raise _StopTraining(SignalInterrupt(sig_all))
+
+    boundary.count = 0
+    boundary.count_sum = 0.0
+    emb_dim = margs.dim
+    exit_code = 0
 
     try:
         while training_step < args.training_steps:
-            if args.raise_error and training_step == args.error_step:
-                raise InjectedFault()
+            # ---- step boundary: fetch the batch, then agree with every rank before any compute
+            loader_at[training_step] = loader.state_dict()
+            loader_at.pop(training_step - 8, None)
+            batch = None
+            try:
+                if args.raise_error and training_step == args.error_step:
+                    raise InjectedFault()
+                fault.fire(training_step, "kill")
+                fault.fire(training_step, "hang")
+                fault.fire(training_step, "data")
+                batch = next(loader)
+                done = ckpt["engine"].poll() if ckpt["engine"] is not None else None
+                if done is not None:
+                    logger.info(f"Checkpoint written: {done.path} ({done.bytes / 1e9:.2f} GB, "
+                                f"stall {done.stall_s:.3f}s, durable after {done.total_s:.2f}s)")
+            except Exception as e:  # noqa: BLE001 - becomes this rank's vote for the error path
+                if pending_err is None:
+                    pending_err = e
+            boundary.count = float(batch.num_items) if batch is not None else 0.0
+            boundary()
+            if batch is None:  # unreachable: a local error always stops every rank above
+                raise RuntimeError("no batch")
+
             if prof_range is not None and training_step == prof_range[0] and prof is None:
                 acts = [torch.profiler.ProfilerActivity.CPU]
                 if device.type == "cuda":
                     acts.append(torch.profiler.ProfilerActivity.CUDA)
                 prof = torch.profiler.profile(activities=acts, record_shapes=True)
                 prof.__enter__()
-            batch = next(loader)
-            tok = batch.inputs.to(device, non_blocking=True)
-            lab = batch.labels.to(device, non_blocking=True)
+
+            # ---- compute: K micro-batches, collectives in the last backward, optimizer, schedule
             if inv_static is not None:
                 inv = inv_static
             else:
-                cnt = torch.tensor([float(batch.num_items)], dtype=torch.float32)
-                cnt = cnt.to(device, non_blocking=True)
-                if info.distributed:
-                    torch.distributed.all_reduce(cnt)
-                inv = cnt.clamp_min(1.0).reciprocal()
-            loss = model(tok, lab, inv)
-            loss.backward()
-            reducer.finish()
-            optimizer.clip_grad_norm_(args.grad_max_norm)
-            if ckpt["engine"] is not None:
-                ckpt["engine"].fence()
-            lr_now = optimizer.param_groups[0]["lr"]
-            optimizer.step()
-            lr_scheduler.step()
+                c = torch.tensor([max(1.0, boundary.count_sum)], dtype=torch.float64).reciprocal_().float()
+                inv = c.to(device, non_blocking=True)
+            tok_all = batch.inputs.to(device, non_blocking=True)
+            lab_all = batch.labels.to(device, non_blocking=True)
+            phase = "forward"
+            loss = None
+            try:
+                for k in range(K):
+                    reducer.begin_micro(k, K)
+                    tok, lab = tok_all[k * B : (k + 1) * B], lab_all[k * B : (k + 1) * B]
+                    fault.fire(training_step, "forward")
+                    if k == K - 1 and fault.at(training_step, "backward"):
+                        reducer.fault_after_buckets = 1
+                    lk = model(tok, lab, inv)
+                    phase = "backward"
+                    lk.backward()
+                    loss = lk.detach() if loss is None else loss + lk.detach()
+                    phase = "forward"
+                phase = "finish"
+                reducer.finish()
+                phase = "optimizer"
+                fault.fire(training_step, "optimizer")
+                optimizer.clip_grad_norm_(args.grad_max_norm)
+                if ckpt["engine"] is not None:
+                    ckpt["engine"].fence()
+                lr_now = optimizer.param_groups[0]["lr"]
+                phase = "step"
+                optimizer.step()
+                phase = "schedule"
+                lr_scheduler.step()
+                phase = "post"
+                fault.fire(training_step, "post")
+            except Exception as e:  # noqa: BLE001
+                logger.error(f"Training error at step {training_step} ({phase}): {e!r}")
+                pending_err = e
+                reducer.fault_after_buckets = 0
+                try:
+                    _complete_step(phase, reducer, optimizer, lr_scheduler, (K * B, S), emb_dim)
+                except Exception as e2:  # noqa: BLE001
+                    raise _FatalStepError(f"could not complete step {training_step} after {e!r}: {e2!r}") from e2
+                lr_now = optimizer.param_groups[0]["lr"]
             steps_window += 1
 
-            if training_step == 1 or training_step % args.logging_frequency == 0:
+            if pending_err is None and (training_step == 1 or training_step % args.logging_frequency == 0):
                 extra = {"lr": f"{lr_now:.3e}"}
                 if device.type == "cuda":
                     extra["peak_HBM_GB"] = f"{torch.cuda.max_memory_allocated(device) / 2**30:.1f}"
-                if info.distributed:
-                    # each rank's loss is its token sum over the GLOBAL token count: the
-                    # logged global-batch mean is their sum (every rank logs at the same steps)
-                    loss = loss.detach().clone()
-                    torch.distributed.all_reduce(loss)
                 losslog.push(training_step, loss, extra, norm=optimizer.norm_for_logging())
                 if metrics_f is not None:
                     now = time.perf_counter()
@@ -377,60 +542,101 @@ def train(args) -> int:
                 prof.export_chrome_trace(out)
                 logger.info(f"torch.profiler trace written to {out}")
                 prof, prof_range = None, None
-            losslog.flush()
-            optimizer.check_finite(block=False)  # deferred non-finite check → error path
-            done = ckpt["engine"].poll() if ckpt["engine"] is not None else None
-            if done is not None:
-                logger.info(f"Checkpoint written: {done.path} ({done.bytes / 1e9:.2f} GB, "
-                            f"stall {done.stall_s:.3f}s, durable after {done.total_s:.2f}s)")
-            if args.save_every and training_step % args.save_every == 0 and training_step < args.training_steps:
-                save_checkpoint(blocking=args.no_async_checkpoint)
-            if args.consensus_every <= 1 or training_step % args.consensus_every == 0:
-                sig = monitor.pending()
-                if info.distributed:
-                    sig = fdist.ctrl_allreduce_max(sig)
-                if sig:
-                    raise SignalInterrupt(sig)
-        losslog.flush(force=True)
-        if device.type == "cuda":
-            torch.cuda.synchronize()
-        optimizer.check_finite(block=True)
+            if (pending_err is None and args.save_every and training_step % args.save_every == 0
+                    and training_step < args.training_steps):
+                save_checkpoint(blocking=args.no_async_checkpoint, step_now=training_step)
+        boundary.count = 0.0
+        boundary(final=True)  # drains the loss log, last non-finite check, last signals
         if ckpt["engine"] is not None:
             ckpt["engine"].wait()
         logger.info("Training completed")
-    except Exception as e:  # noqa: BLE001 - the reference catches everything here (train.py:121)
-        losslog.flush(force=True)
+    except _StopTraining as stop:
+        e = stop.cause
         exit_type = classify_exception(e)
-        if exit_type == -1 and not isinstance(e, InjectedFault):
-            logger.error(f"Training error: {e!r}")
-        # signals are agreed across ranks; the injected fault fires on every rank at
-        # the same step; any other error may be local to this rank
-        collective = info.distributed and isinstance(e, (SignalInterrupt, InjectedFault))
         try:
             if ckpt["engine"] is not None:
                 ckpt["engine"].wait()
         except Exception as we:  # noqa: BLE001
             logger.error(f"previous checkpoint write failed: {we!r}")
+        step_now = training_step
 
         def _save():
             with monitor.blocked():
-                st = save_checkpoint(blocking=True, collective=collective or not info.distributed)
-            if st is False:
-                return False
+                st = save_checkpoint(blocking=True, step_now=step_now)
             if st is not None:
                 logger.info(f"Checkpoint {st.path}: {st.bytes / 1e9:.2f} GB in {st.total_s:.2f}s "
                             f"(mode {st.mode})")
 
-        handle_exit(_save, training_step, exit_type, logger, job_id=job_id,
-                    sbatch_script=args.sbatch_script, is_main=info.is_main)
+        if exit_type == -1 and not isinstance(e, InjectedFault) and info.is_main:
+            logger.error(f"Training error: {e!r}")
+        handle_exit(_save, step_now, exit_type, logger, job_id=job_id,
+                    sbatch_script=args.sbatch_script, is_main=info.is_main, rank=info.rank)
+    except (fdist.PeerFailure, _FatalStepError) as e:
+        # a peer vanished (or this rank cannot finish its share of a step): no collective
+        # is possible any more. A survivor with complete, replicated state writes the
+        # checkpoint alone; then exit non-zero at once (process-group teardown could block
+        # on collectives that will never complete).
+        logger.error(f"[EXIT HANDLER] Lost a peer rank: {e}")
+        step_now = training_step
+        complete = isinstance(e, fdist.PeerFailure) and pending_err is None
+        if complete and info.distributed and device.type == "cuda" and not _drained(device, 0.5 * info.peer_timeout_s):
+            logger.error("[EXIT HANDLER] the last step's collectives never completed; no complete state to save")
+            complete = False
+        if complete and info.distributed:
+            try:
+                rollback_to_first_bad()
+                step_now = training_step
+                with monitor.blocked():
+                    st = save_solo(step_now)
+                if st:
+                    logger.error(f"[rank {info.rank}] [EXIT HANDLER] Checkpoint saved at step {step_now}")
+            except Exception as se:  # noqa: BLE001
+                logger.error(f"[EXIT HANDLER] Checkpoint could not be saved at step {step_now}: {se!r}")
+        exit_code = 1
     finally:
         loader.close()
         if metrics_f is not None:
             metrics_f.close()
         monitor.uninstall()
+        if ckpt["engine"] is not None and not exit_code:
+            ckpt["engine"].preallocated(None)  # never exit while the pinning thread is inside hipHostMalloc
     sys.stdout.flush()
     sys.stderr.flush()
+    if exit_code:
+        for h in logger.handlers:
+            h.flush()
+        os._exit(exit_code)
     return 0
+
+
+def _drained(device: torch.device, timeout_s: float) -> bool:
+    """Wait (bounded) until every stream of ``device`` has finished its queued work: a
+    collective whose peer died never completes, and a plain device sync would block forever."""
+    import threading
+
+    t = threading.Thread(target=torch.cuda.synchronize, args=(device,), daemon=True)
+    t.start()
+    t.join(timeout_s)
+    return not t.is_alive()
+
+
+def _complete_step(phase: str, reducer, optimizer, lr_scheduler, tokens_shape, dim: int) -> None:
+    """After a failure at ``phase``, finish this rank's share of the step so the peers'
+    collectives complete: unlaunched buckets go out poisoned (NaN), so every rank's
+    non-finite guard skips the step's update; then the optimizer/scheduler steps run as
+    on the peers. Failures before backward's last bucket poison the whole step; a
+    failure after ``optimizer.step()`` was enqueued leaves a valid, complete step."""
+    if phase in ("forward", "backward", "finish", "optimizer"):
+        # at "optimizer" the gradients are complete and every bucket went out with valid
+        # data: the peers' step is valid, so this rank takes the same valid step
+        if phase != "optimizer":
+            reducer.poison_and_complete(tokens_shape, dim)
+        optimizer.step()
+        lr_scheduler.step()
+    elif phase == "step":
+        raise RuntimeError("failure inside optimizer.step(): its collectives may be half issued")
+    elif phase == "schedule":
+        lr_scheduler.step()
 
 
 def main(argv=None) -> None:

@@ -171,7 +171,22 @@ def build_parser() -> argparse.ArgumentParser:
         "--consensus-every",
         type=int,
         default=1,
-        help="Agree on pending stop signals across ranks every N steps",
+        help="(kept for compatibility) the ranks now vote at every step boundary: signals, rank-local "
+        "errors and non-finite gradients must stop every rank at the same step",
+    )
+    parser.add_argument(
+        "--grad-accum",
+        type=int,
+        default=1,
+        help="Gradient accumulation: micro-batches of --batch-size per optimizer step (collectives only "
+        "in the last micro-batch's backward)",
+    )
+    parser.add_argument(
+        "--peer-timeout",
+        type=float,
+        default=60.0,
+        help="Seconds a rank waits at the per-step vote for a silent peer before declaring it lost "
+        "(a dead peer is detected at once); well under Slurm's 120 s USR1 lead",
     )
     parser.add_argument(
         "--flash-bwd",

@@ -21,3 +21,15 @@ def linear_warmup_constant(warmup_steps: int, current_step: int) -> float:
 
 def build_lr_scheduler(optimizer, warmup_steps: int) -> LambdaLR:
     return LambdaLR(optimizer, functools.partial(linear_warmup_constant, warmup_steps))
+
+
+def rollback_lr_scheduler(sched: LambdaLR, k: int) -> None:
+    """Undo the last ``k`` ``sched.step()`` calls (steps whose optimizer update was skipped
+    by the non-finite guard and are rolled back by the trainer)."""
+    if k <= 0:
+        return
+    sched.last_epoch -= k
+    lrs = [base * lam(sched.last_epoch) for base, lam in zip(sched.base_lrs, sched.lr_lambdas)]
+    for g, lr in zip(sched.optimizer.param_groups, lrs):
+        g["lr"] = lr
+    sched._last_lr = lrs

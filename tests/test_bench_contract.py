@@ -66,3 +66,16 @@ def test_bench_torchrun_two_ranks(mode):
     assert j["n_gpus"] == 2 and j["config"]["parallelism"] == "dp2" and j["config"]["global_batch"] == 2
     assert j["grad_mode"] == mode
     assert abs(j["value"] - 2 * 64 / (j["ms_per_step"] / 1e3)) / j["value"] < 0.02
+    # vs_baseline is per GPU (the metric is tokens/sec/GPU): it does not scale with N by itself
+    assert abs(j["vs_baseline"] - j["tokens_per_s_per_gpu"] / 6376.0) < 1e-3
+    assert "exposed_comm_ms_per_step" in j and "compute_only_ms_per_step" in j
+
+
+def test_bench_grad_accum_two_ranks():
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2", "--grad-accum", "2"] + ARGS
+    r = subprocess.run(cmd, cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    j = _json_lines(r.stdout)[0]
+    assert j["config"]["global_batch"] == 4 and j["grad_accum"] == 2
+    assert abs(j["value"] - 4 * 64 / (j["ms_per_step"] / 1e3)) / j["value"] < 0.02

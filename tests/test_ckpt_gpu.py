@@ -48,7 +48,13 @@ def test_background_pinned_preallocation(tmp_path):
     path = str(tmp_path / "p.ckpt")
     # the save may race the thread: it blocks on the host-buffer lock, then uses the same buffers
     st = eng.save(path, lambda h: {"m": h["params"], "a": h["exp_avg"], "v": h["exp_avg_sq"]}, blocking=True)
-    assert eng.preallocated(0) and eng.prealloc_s is not None
+    assert eng.preallocated(30) and eng.prealloc_s is not None
+    host_before = {k: v.data_ptr() for k, v in eng.host_views().items()}
+    st2 = eng.save(path, lambda h: {"m": h["params"], "a": h["exp_avg"], "v": h["exp_avg_sq"]}, blocking=True)
+    assert st2.mode == st.mode
+    # the second save reuses the pinned buffers (no new allocation) and the event pool
+    assert {k: v.data_ptr() for k, v in eng.host_views().items()} == host_before
+    assert eng._eng is None or eng._eng.num_events() <= 3
     assert eng.mode in ("hbm", "host") and st.mode == eng.mode
     assert all(t.is_pinned() for t in eng.host_views().values())
     c = load_checkpoint(path)

@@ -189,3 +189,72 @@ def test_resume_dp2_checkpoint_on_one_rank_and_back(tmp_path):
     assert "written by 2 ranks, resuming on 1" in out
     rc, out = _run(d, "402", base + ["--checkpoint-id", "401", "--raise-error", "--error-step", "12"])
     assert rc == 0 and "Resuming training from training_step 9" in out and "Checkpoint saved at step 12" in out, out
+
+
+def _accum_worker(rank, world, port, out_dir, mode, K):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from fault_tolerant_llm_training_amd.data.synthetic import SyntheticTokens
+    from fault_tolerant_llm_training_amd.models.llama import build_model, model_args_for
+    from fault_tolerant_llm_training_amd.parallel.ddp import GradReducer
+
+    a = model_args_for("tiny", vocab_size=128, seq_len=16)
+    m = build_model(a, "cpu", torch.float32, seed=5)
+    ddp = GradReducer(m.flat, m.sinks_in_backward_order(), bucket_mb=0.05, mode=mode)
+    ds = SyntheticTokens(128, 16, seed=9, rank=rank, world_size=world, pin=False)
+    x, y = ds.batch(0, K)  # this rank's K micro-batches of one sequence each
+    y[0, :3] = -100
+    n = torch.tensor([float((y != -100).sum())])
+    dist.all_reduce(n)
+    calls = []
+    orig = ddp._launch_now
+    ddp._launch_now = lambda b: (calls.append(b.idx), orig(b))[1]
+    for k in range(K):
+        ddp.begin_micro(k, K)
+        loss = m(x[k : k + 1], y[k : k + 1], 1.0 / n)
+        loss.backward()
+        if k < K - 1:
+            assert calls == [], "no collective before the last micro-batch"
+    ddp.finish()
+    assert calls == sorted(calls) and len(calls) == len(ddp.buckets), calls  # in-order launches
+    full = torch.full_like(m.flat.grads, float("nan"))
+    for b in ddp.buckets:
+        if mode == "zero1" and not b.sparse:
+            lo = b.lo + rank * b.shard_len
+            full[lo : lo + b.shard_len] = ddp.grad_for_update(b)
+        elif mode == "zero1":
+            lo = b.lo + rank * b.shard_len
+            full[lo : lo + b.shard_len] = m.flat.grads[lo : lo + b.shard_len]
+        else:
+            full[b.lo : b.hi] = m.flat.grads[b.lo : b.hi]
+    torch.save(full, os.path.join(out_dir, f"a{rank}.pt"))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode", ["allreduce", "zero1"])
+def test_grad_accumulation_equals_global_batch(tmp_path, mode):
+    """--grad-accum K: K micro-batches per rank, collectives only in the last backward (sparse
+    embedding rows of all micro-batches exchanged at once) == one process on the global batch."""
+    world, K = 2, 2
+    mp.start_processes(_accum_worker, args=(world, _free_port(), str(tmp_path), mode, K), nprocs=world,
+                       start_method="spawn")
+    gs = [torch.load(tmp_path / f"a{r}.pt") for r in range(world)]
+    g0 = gs[0]
+    for g in gs[1:]:
+        g0 = torch.where(torch.isnan(g0), g, g0)
+    assert not torch.isnan(g0).any()
+    from fault_tolerant_llm_training_amd.data.synthetic import SyntheticTokens
+    from fault_tolerant_llm_training_amd.models.llama import build_model, model_args_for
+
+    a = model_args_for("tiny", vocab_size=128, seq_len=16)
+    m = build_model(a, "cpu", torch.float32, seed=5)
+    xs, ys = [], []
+    for r in range(world):
+        x, y = SyntheticTokens(128, 16, seed=9, rank=r, world_size=world, pin=False).batch(0, K)
+        y[0, :3] = -100
+        xs.append(x)
+        ys.append(y)
+    loss = m(torch.cat(xs), torch.cat(ys))
+    loss.backward()
+    assert torch.allclose(g0, m.flat.grads, atol=2e-6, rtol=1e-4)
