@@ -28,6 +28,56 @@ from .grad_sink import GradSink
 
 IGNORE_INDEX = -100
 
+# GEMM backend per product: the hand-written gfx950 kernel (csrc/kernels/gemm.hip) reads every
+# operand in its row-major layout (no transposes) and fuses SwiGLU into the FFN GEMMs;
+# hipBLASLt (torch.mm) is kept where it measures faster. FT_GEMM = "auto" (per-product policy
+# below, from scripts/gemm_bench.py on MI355X), "hand" (every fitting shape), "blas" (none).
+_GEMM_MODE = os.environ.get("FT_GEMM", "auto")
+# products the hand kernel takes in "auto" (FT_GEMM_AUTO, comma list of fwd,dx,dw,ffn).
+# Default: none. Measured on the Llama-3-8B step (profiles/r2_gemm_hand_vs_hipblaslt.md): the
+# hand kernel runs each product at 0.72-0.95x of hipBLASLt, and the whole step at 109.4 ms
+# (all hipBLASLt) vs 112.9 (SwiGLU-fused FFN on the hand kernel), 113.7 (dW), 118.8 (both),
+# 123.1 (every product) — the transposes and SwiGLU passes it removes cost less than the GEMM
+# speed it gives up.
+_HAND_AUTO = set(k for k in os.environ.get("FT_GEMM_AUTO", "").split(",") if k)
+
+
+def set_gemm_mode(mode: str) -> None:
+    global _GEMM_MODE
+    if mode not in ("auto", "hand", "blas"):
+        raise ValueError(mode)
+    _GEMM_MODE = mode
+
+
+def _hand(kind: str, M: int, N: int, K: int, *ts) -> bool:
+    """Use the hand GEMM for product ``kind`` ("fwd", "dx", "dw", "ffn") of shape M x N x K?"""
+    if _GEMM_MODE == "blas" or not all(t.is_cuda and t.dtype == torch.bfloat16 for t in ts):
+        return False
+    if M % 256 or N % 256 or K % 64:
+        return False
+    return _GEMM_MODE == "hand" or kind in _HAND_AUTO
+
+
+def mm_fwd(x2: torch.Tensor, w: torch.Tensor, residual: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """y = x2 @ w^T (+ residual): x2 [T, K], w [N, K] (nn.Linear layout)."""
+    T, K = x2.shape
+    N = w.shape[0]
+    if _hand("fwd", T, N, K, x2, w):
+        return kernels().gemm(x2.contiguous(), True, w, True, T, N, K, None,
+                              None if residual is None else residual.reshape(T, N).contiguous(), False, 0)
+    if residual is None:
+        return torch.mm(x2, w.t())
+    return torch.addmm(residual.reshape(T, N), x2, w.t())
+
+
+def mm_dx(dy2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """dx = dy2 @ w: dy2 [T, N], w [N, K]."""
+    T, N = dy2.shape
+    K = w.shape[1]
+    if _hand("dx", T, K, N, dy2, w):
+        return kernels().gemm(dy2.contiguous(), True, w, False, T, K, N, None, None, False, 0)
+    return torch.mm(dy2, w)
+
 # Weight gradients dW = dY^T X as a K-contiguous ("TN") GEMM on transposed copies of
 # both operands: hipBLASLt runs that layout ~1.3x faster on MI355X than the
 # token-major ("NT") product of the row-major activations, and the gfx950
@@ -57,6 +107,17 @@ def weight_grad(dy2: torch.Tensor, x2: torch.Tensor, sink: Optional[GradSink],
     ``bufs``: preallocated (dyT, xT) outputs for the transposes (see weight_grad_async)."""
     if xT is not None and x2 is None:
         x2 = xT.t()
+    T, N = dy2.shape
+    K = x2.shape[1]
+    if _hand("dw", N, K, T, dy2, x2) and dy2.is_contiguous() and x2.is_contiguous():
+        # dW[N, K] = dY^T X read straight from the row-major dY [T, N] and X [T, K]
+        out = sink.buf.view(N, K) if sink is not None else None
+        acc = sink.accumulate if sink is not None else False
+        r = kernels().gemm(dy2, False, x2, False, N, K, T, out, None, acc, 0)
+        if sink is not None:
+            sink.ready()
+            return None
+        return r
     if _use_tn(dy2, x2):
         K_ = kernels()
         ba, bb = bufs if bufs is not None else (None, None)
@@ -121,7 +182,7 @@ def weight_grad_async(dy2: torch.Tensor, x2: Optional[torch.Tensor], sink: Optio
     x2 = x2.contiguous() if x2 is not None else None
     xx = x2 if x2 is not None else xT.t()
     bufs = None
-    if _use_tn(dy2, xx):
+    if _use_tn(dy2, xx) and not _hand("dw", dy2.shape[1], xx.shape[1], dy2.shape[0], dy2, xx):
         T, N = dy2.shape
         bufs = (dy2.new_empty((N, T)) if dyT is None else None,
                 xx.new_empty((xx.shape[1], T)) if xT is None else None)
@@ -319,10 +380,7 @@ class LinearFn(torch.autograd.Function):
         K = x.shape[-1]
         N = weight.shape[0]
         x2 = x.reshape(-1, K)
-        if residual is None:
-            y = torch.mm(x2, weight.t())
-        else:
-            y = torch.addmm(residual.reshape(-1, N), x2, weight.t())
+        y = mm_fwd(x2, weight, residual)
         ctx.sink = sink
         ctx.has_res = residual is not None
         ctx.xshape = x.shape
@@ -337,7 +395,7 @@ class LinearFn(torch.autograd.Function):
         dw = None
         # weight gradient first, so its all-reduce bucket can launch while dx runs
         dw = weight_grad_async(dy2, x2, ctx.sink)
-        dx = torch.mm(dy2, w).view(ctx.xshape)
+        dx = mm_dx(dy2, w).view(ctx.xshape)
         return dx, dw, None, (dy if ctx.has_res else None)
 
 
@@ -506,10 +564,49 @@ class FeedForwardFn(torch.autograd.Function):
         return dx, dw13, dw2, None, None
 
 
+class FusedFFNFn(torch.autograd.Function):
+    """FFN on the hand GEMM with SwiGLU in the GEMM epilogues (csrc/kernels/gemm.hip):
+
+    forward   (a, gu) = gemm_swiglu(x, w13)      a = silu(g) * u, gu = [g | u] kept for backward
+              y = a @ w2^T
+    backward  dW2 = dy^T a                       (row-major operands, no transpose)
+              dgu = gemm_swiglu_bwd(dy, w2, gu)  da = dy @ w2 and the SwiGLU backward in one kernel
+              dW13 = dgu^T x ; dx = dgu @ w13
+    No separate activation kernel and no transposed copies. Reference math: model.py:253-254."""
+
+    @staticmethod
+    def forward(ctx, x, w13, w2, sink13, sink2):
+        K_ = kernels()
+        D = x.shape[-1]
+        x2 = x.reshape(-1, D).contiguous()
+        a, gu = K_.gemm_swiglu(x2, w13)
+        y = mm_fwd(a, w2)
+        ctx.sinks = (sink13, sink2)
+        ctx.xshape = x.shape
+        ctx.save_for_backward(x2, gu, a, w13, w2)
+        return y.view(*x.shape[:-1], w2.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, gu, a, w13, w2 = ctx.saved_tensors
+        sink13, sink2 = ctx.sinks
+        dy2 = dy.reshape(-1, w2.shape[0]).contiguous()
+        dw2 = weight_grad_async(dy2, a, sink2)
+        dgu = kernels().gemm_swiglu_bwd(dy2, w2, gu)
+        dw13 = weight_grad_async(dgu, x2, sink13)
+        dx = mm_dx(dgu, w13).view(ctx.xshape)
+        return dx, dw13, dw2, None, None
+
+
 def feed_forward(x, w13, w2, sink13=None, sink2=None):
     """SwiGLU FFN on the fused [w1; w3] weight; fused node on the GPU, composed ops on CPU."""
-    if _FUSED_FFN and x.is_cuda and w13.shape[0] % 128 == 0 and x.numel() // x.shape[-1] % 64 == 0:
-        return FeedForwardFn.apply(x, w13, w2, sink13, sink2)
+    if x.is_cuda and _FUSED_FFN:
+        T, D = x.numel() // x.shape[-1], x.shape[-1]
+        F = w13.shape[0] // 2
+        if _hand("ffn", T, 2 * F, D, x, w13, w2) and F % 256 == 0:
+            return FusedFFNFn.apply(x, w13, w2, sink13, sink2)
+        if w13.shape[0] % 128 == 0 and T % 64 == 0:
+            return FeedForwardFn.apply(x, w13, w2, sink13, sink2)
     return linear(swiglu(linear(x, w13, sink13)), w2, sink2)
 
 
@@ -525,7 +622,7 @@ class LMHeadCrossEntropyFn(torch.autograd.Function):
         ctx.sink = sink
         ctx.hshape = h.shape
         if h.is_cuda:
-            logits = torch.mm(h2, weight.t())
+            logits = mm_fwd(h2.contiguous(), weight)
             loss_rows, lse = kernels().xent_fwd(logits, lab.contiguous(), IGNORE_INDEX)
             loss = loss_rows.sum() * inv_count
             ctx.save_for_backward(h2, weight, logits, lse, lab, inv_count)
@@ -544,7 +641,7 @@ class LMHeadCrossEntropyFn(torch.autograd.Function):
             kernels().xent_bwd_(logits, lab, lse, gf, inv_count.float().reshape(1).contiguous(), IGNORE_INDEX)
             dlogits = logits  # overwritten in place
             dw = weight_grad_async(dlogits, h2, sink)
-            dh = torch.mm(dlogits, w).view(ctx.hshape)
+            dh = mm_dx(dlogits, w).view(ctx.hshape)
             return dh, dw, None, None, None
         h2, w, lab, inv_count = ctx.saved_tensors
         with torch.enable_grad():
