@@ -90,7 +90,36 @@ __global__ __launch_bounds__(256) void xent_bwd_kernel(bf16_t* __restrict__ logi
   }
 }
 
+// x *= g[0] unless g[0] == 1 (then every block exits at once): the upstream gradient of a
+// loss whose input gradients were already formed in the forward pass (fused LM head).
+__global__ __launch_bounds__(256) void scale_by_kernel(bf16_t* __restrict__ x, long n8,
+                                                       const float* __restrict__ g) {
+  const float s = g[0];
+  if (s == 1.f) return;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n8; i += (long)gridDim.x * 256) {
+    float v[8];
+    unpack8(reinterpret_cast<const uint4*>(x)[i], v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] *= s;
+    reinterpret_cast<uint4*>(x)[i] = pack8(v);
+  }
+}
+
 }  // namespace
+
+void scale_by_(const at::Tensor& x, const at::Tensor& g) {
+  FT_CHECK_CUDA(x);
+  FT_CHECK_BF16(x);
+  FT_CHECK_CONTIG(x);
+  FT_CHECK_F32(g);
+  TORCH_CHECK(x.numel() % 8 == 0, "scale_by_: numel must be a multiple of 8");
+  const at::DeviceGuard guard(x.device());
+  const long n8 = x.numel() / 8;
+  if (n8 > 0)
+    hipLaunchKernelGGL(scale_by_kernel, dim3((unsigned)std::min<long>((n8 + 255) / 256, 2048)), dim3(256), 0,
+                       ft_stream(), mptr<bf16_t>(x), n8, cptr<float>(g));
+  FT_LAUNCH_CHECK();
+}
 
 // Returns (per-row loss [T] fp32, lse [T] fp32).
 std::tuple<at::Tensor, at::Tensor> xent_fwd(const at::Tensor& logits, const at::Tensor& labels,
@@ -135,6 +164,7 @@ void xent_bwd_(const at::Tensor& logits, const at::Tensor& labels, const at::Ten
 }
 
 TORCH_LIBRARY_FRAGMENT(ftamd, m) {
+  m.def("scale_by_(Tensor(a!) x, Tensor g) -> ()", &scale_by_);
   m.def("xent_fwd(Tensor logits, Tensor labels, int ignore_index) -> (Tensor, Tensor)", &xent_fwd);
   m.def(
       "xent_bwd_(Tensor(a!) logits, Tensor labels, Tensor lse, Tensor grad, Tensor inv_count, int "

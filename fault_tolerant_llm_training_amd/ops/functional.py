@@ -613,7 +613,72 @@ def feed_forward(x, w13, w2, sink13=None, sink2=None):
 # --------------------------------------------------------------------------------------
 # LM head + cross-entropy (sum over tokens × 1/num_items)
 # --------------------------------------------------------------------------------------
+# Token rows per LM-head chunk: the [rows, V] bf16 logits of one chunk stay under this many MiB.
+# Default 1 GiB: with V = 131072, seq 2048 (512 MiB of logits) runs as one chunk and seq 65536
+# in 16 chunks of 4096 rows instead of a 16 GiB [T, V] logits tensor plus its gradient. On a
+# 288 GB MI355X the half-GiB at seq 2048 is cheaper to keep than to split: two 256 MiB chunks
+# measured 109.7 vs 107.5 ms/step (profiles/r2_head_chunk_ab.log) — the dX GEMM at M = 1024
+# fills the chip worse and dW is accumulated twice.
+_HEAD_CHUNK_MB = float(os.environ.get("FT_HEAD_CHUNK_MB", "1024"))
+
+
+def _head_rows(T: int, V: int) -> int:
+    rows = int(_HEAD_CHUNK_MB * 2**20) // (2 * V)
+    rows = max(256, rows // 256 * 256)
+    return min(T, rows)
+
+
+# The head's dW from a chunk of dlogits: hipBLASLt on the row-major operands (no transposed
+# copy of the 256 MiB chunk, which would double the chunk's footprint); FT_HEAD_DW_TN=1 uses
+# the transposed ("TN") layout instead.
+_HEAD_DW_TN = os.environ.get("FT_HEAD_DW_TN", "0") == "1"
+
+
+def _dx_into(out: torch.Tensor, dy2: torch.Tensor, w: torch.Tensor) -> None:
+    """out[T, K] = dy2[T, N] @ w[N, K]."""
+    T, N = dy2.shape
+    K = w.shape[1]
+    if _hand("dx", T, K, N, dy2, w):
+        kernels().gemm(dy2, True, w, False, T, K, N, out, None, False, 0)
+    else:
+        torch.mm(dy2, w, out=out)
+
+
+def _dw_into(out: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor, accumulate: bool) -> None:
+    """out[N, K] (+)= dy2[T, N]^T @ x2[T, K]."""
+    T, N = dy2.shape
+    K = x2.shape[1]
+    if _hand("dw", N, K, T, dy2, x2):
+        kernels().gemm(dy2, False, x2, False, N, K, T, out, None, accumulate, 0)
+        return
+    if _HEAD_DW_TN and _use_tn(dy2, x2):
+        K_ = kernels()
+        a, b = K_.transpose2d(dy2, None), K_.transpose2d(x2, None)
+        if accumulate:
+            out.addmm_(a, b.t())
+        else:
+            torch.mm(a, b.t(), out=out)
+        return
+    if accumulate:
+        out.addmm_(dy2.t(), x2)
+    else:
+        torch.mm(dy2.t(), x2, out=out)
+
+
 class LMHeadCrossEntropyFn(torch.autograd.Function):
+    """LM head + cross-entropy, chunked over token rows, gradients formed in the forward pass.
+
+    Reference: logits = h @ W^T (model.py:379), then CE over the fp32 copy of the full
+    [T, V] logits (train.py:101-102). Here, per chunk of rows (``_head_rows``): logits_c
+    = h_c W^T (bf16), per-row log-sum-exp + NLL (xent_fwd), dlogits written in place
+    (xent_bwd_, scaled by 1/num_items), then dh_c = dlogits_c W and dW (+)= dlogits_c^T h_c
+    straight into the flat gradient buffer; the chunk's logits are freed before the next.
+    Backward only applies the upstream gradient (a no-op kernel when it is 1, which it is
+    for ``loss.backward()``) and marks the weight gradient ready. Under gradient
+    accumulation (the sink already holds earlier micro-batches) the forward keeps only the
+    per-row lse and backward recomputes each chunk's logits with the upstream gradient.
+    """
+
     @staticmethod
     def forward(ctx, h, weight, sink, labels, inv_count):
         D = h.shape[-1]
@@ -621,36 +686,87 @@ class LMHeadCrossEntropyFn(torch.autograd.Function):
         lab = labels.reshape(-1)
         ctx.sink = sink
         ctx.hshape = h.shape
-        if h.is_cuda:
-            logits = mm_fwd(h2.contiguous(), weight)
-            loss_rows, lse = kernels().xent_fwd(logits, lab.contiguous(), IGNORE_INDEX)
-            loss = loss_rows.sum() * inv_count
-            ctx.save_for_backward(h2, weight, logits, lse, lab, inv_count)
+        if not h.is_cuda:
+            logits = torch.mm(h2, weight.t())
+            loss = F.cross_entropy(logits.float(), lab, reduction="sum", ignore_index=IGNORE_INDEX) * inv_count
+            ctx.save_for_backward(h2, weight, lab, inv_count)
             return loss
-        logits = torch.mm(h2, weight.t())
-        loss = F.cross_entropy(logits.float(), lab, reduction="sum", ignore_index=IGNORE_INDEX) * inv_count
-        ctx.save_for_backward(h2, weight, lab, inv_count)
+        K_ = kernels()
+        h2 = h2.contiguous()
+        lab = lab.contiguous()
+        T, V = h2.shape[0], weight.shape[0]
+        rows = _head_rows(T, V)
+        need = ctx.needs_input_grad[0] or ctx.needs_input_grad[1] or sink is not None
+        fused = need and not (sink is not None and sink.accumulate)
+        ctx.fused = fused
+        ctx.rows = rows
+        inv = inv_count.float().reshape(1).contiguous()
+        one = torch.ones(1, dtype=torch.float32, device=h.device)
+        dh = torch.empty_like(h2) if fused else None
+        dw = None
+        if fused:
+            dw = sink.buf.view(V, D) if sink is not None else torch.empty_like(weight)
+        losses, lses = [], []
+        for c, r0 in enumerate(range(0, T, rows)):
+            hc, lc = h2[r0 : r0 + rows], lab[r0 : r0 + rows]
+            logits = mm_fwd(hc, weight)
+            lr, lse = K_.xent_fwd(logits, lc, IGNORE_INDEX)
+            losses.append(lr)
+            if fused:
+                K_.xent_bwd_(logits, lc, lse, one, inv, IGNORE_INDEX)  # logits := dlogits
+                _dx_into(dh[r0 : r0 + rows], logits, weight)
+                _dw_into(dw, logits, hc, c > 0)
+            else:
+                lses.append(lse)
+            del logits
+        loss = (losses[0] if len(losses) == 1 else torch.cat(losses)).sum() * inv_count
+        if fused:
+            ctx.save_for_backward(dh, dw if sink is None else None)
+        else:
+            ctx.save_for_backward(h2, weight, lab, inv, torch.cat(lses))
         return loss
 
     @staticmethod
     def backward(ctx, g):
         sink = ctx.sink
-        if g.is_cuda:
-            h2, w, logits, lse, lab, inv_count = ctx.saved_tensors
-            gf = g.detach().float().reshape(1).contiguous()
-            kernels().xent_bwd_(logits, lab, lse, gf, inv_count.float().reshape(1).contiguous(), IGNORE_INDEX)
-            dlogits = logits  # overwritten in place
-            dw = weight_grad_async(dlogits, h2, sink)
-            dh = mm_dx(dlogits, w).view(ctx.hshape)
-            return dh, dw, None, None, None
-        h2, w, lab, inv_count = ctx.saved_tensors
-        with torch.enable_grad():
-            hr = h2.detach().requires_grad_(True)
-            wr = w.detach().requires_grad_(True)
-            logits = torch.mm(hr, wr.t())
-            loss = F.cross_entropy(logits.float(), lab, reduction="sum", ignore_index=IGNORE_INDEX) * inv_count
-            dh, dw = torch.autograd.grad(loss, (hr, wr), g)
-        return dh.view(ctx.hshape), _write_weight_grad(sink, dw), None, None, None
+        if not g.is_cuda:
+            h2, w, lab, inv_count = ctx.saved_tensors
+            with torch.enable_grad():
+                hr = h2.detach().requires_grad_(True)
+                wr = w.detach().requires_grad_(True)
+                logits = torch.mm(hr, wr.t())
+                loss = F.cross_entropy(logits.float(), lab, reduction="sum", ignore_index=IGNORE_INDEX) * inv_count
+                dh, dw = torch.autograd.grad(loss, (hr, wr), g)
+            return dh.view(ctx.hshape), _write_weight_grad(sink, dw), None, None, None
+        K_ = kernels()
+        gf = g.detach().float().reshape(1).contiguous()
+        if ctx.fused:
+            dh, dw = ctx.saved_tensors
+            K_.scale_by_(dh, gf)
+            if sink is not None:
+                K_.scale_by_(sink.buf, gf)
+                sink.ready()
+                return dh.view(ctx.hshape), None, None, None, None
+            K_.scale_by_(dw, gf)
+            return dh.view(ctx.hshape), dw, None, None, None
+        h2, w, lab, inv, lse = ctx.saved_tensors
+        T, D = h2.shape
+        V = w.shape[0]
+        rows = ctx.rows
+        dh = torch.empty_like(h2)
+        dw = sink.buf.view(V, D) if sink is not None else torch.empty_like(w)
+        acc0 = sink.accumulate if sink is not None else False
+        for c, r0 in enumerate(range(0, T, rows)):
+            hc, lc = h2[r0 : r0 + rows], lab[r0 : r0 + rows]
+            logits = mm_fwd(hc, w)
+            K_.xent_bwd_(logits, lc, lse[r0 : r0 + rows].contiguous(), gf, inv, IGNORE_INDEX)
+            _dx_into(dh[r0 : r0 + rows], logits, w)
+            _dw_into(dw, logits, hc, acc0 or c > 0)
+            del logits
+        if sink is not None:
+            sink.ready()
+            return dh.view(ctx.hshape), None, None, None, None
+        return dh.view(ctx.hshape), dw, None, None, None
 
 
 def lm_head_cross_entropy(h, weight, labels, inv_count, sink=None):
