@@ -177,6 +177,11 @@ def main():
         "comm_GB_per_rank_per_step": round(
             2.0 * (world - 1) / world * sum(b.numel for b in red.buckets if not b.sparse)
             * model.flat.grads.element_size() / 1e9, 2),
+        # sparse embedding exchange: each rank sends its B*S (token, dY row) pairs and receives
+        # the other W-1 ranks' (all-gather)
+        "sparse_emb_GB_received_per_rank_per_step": round(
+            (world - 1) * B * K * S * (margs.dim * model.flat.grads.element_size() + 8) / 1e9, 3)
+        if red.sparse_embedding else 0.0,
         "recompute_layers": model.recompute_layers,
     }
     if dev.type == "cuda":

@@ -456,10 +456,13 @@ void launch(const GemmArgs& a, int splits, hipStream_t s) {
     hipLaunchKernelGGL((gemm_kernel<AK, BKC, EPI, false>), dim3(a.tiles_m * a.tiles_n, splits), dim3(NT), 0, s, a);
 }
 
-// Splits so that tiles x splits reaches about the CU count without slicing K below 1024.
+// Splits so that tiles x splits reaches about the CU count (256) without slicing K below 1024;
+// a tall-K product with few output tiles (GPT-2's LM-head dX: 24 tiles, K = 131072) goes to
+// ~2 workgroups per CU, where the fp32 slabs are still small next to the GEMM.
 int pick_splits(int tiles, int K) {
   int s = 1;
-  while (tiles * s < 200 && (K / (s * 2)) % BK == 0 && K / (s * 2) >= 1024) s *= 2;
+  const int target = tiles < 64 ? 400 : 200;
+  while (tiles * s < target && (K / (s * 2)) % BK == 0 && K / (s * 2) >= 1024) s *= 2;
   return s;
 }
 

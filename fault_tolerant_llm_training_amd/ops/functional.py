@@ -55,7 +55,12 @@ def _hand(kind: str, M: int, N: int, K: int, *ts) -> bool:
         return False
     if M % 256 or N % 256 or K % 64:
         return False
-    return _GEMM_MODE == "hand" or kind in _HAND_AUTO
+    if _GEMM_MODE == "hand" or kind in _HAND_AUTO:
+        return True
+    # tall-K product with few 256x256 output tiles (the LM head's dX for GPT-2-sized models,
+    # [2048 x 768 x 131072]): the hand kernel's split-K fills the chip where hipBLASLt does not
+    # (496 vs 722 us at d=768, 570 vs 889 us at d=1024; profiles/r2_gemm_gpt2_shapes.log)
+    return kind == "dx" and (M // 256) * (N // 256) < 64 and K >= 16384
 
 
 def mm_fwd(x2: torch.Tensor, w: torch.Tensor, residual: Optional[torch.Tensor] = None) -> torch.Tensor:

@@ -29,6 +29,8 @@ def rollback_lr_scheduler(sched: LambdaLR, k: int) -> None:
     if k <= 0:
         return
     sched.last_epoch -= k
+    if hasattr(sched, "_step_count"):
+        sched._step_count -= k
     lrs = [base * lam(sched.last_epoch) for base, lam in zip(sched.base_lrs, sched.lr_lambdas)]
     for g, lr in zip(sched.optimizer.param_groups, lrs):
         g["lr"] = lr

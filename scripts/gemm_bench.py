@@ -48,6 +48,16 @@ cases = [
 ]
 if quick:
     cases = [c for c in cases if c[0] in ("fwd w13", "dX w13", "dW w13", "fwd head")]
+if "--gpt2" in sys.argv:  # GPT-2-small / -medium (d 768 / 1024) at seq 2048, V = 131072
+    cases = []
+    for tag, d, f, qkv, L in (("s", 768, 2048, 2304, 12), ("m", 1024, 2816, 3072, 24)):
+        cases += [(f"{tag} fwd qkv", "nt", T, qkv, d, L), (f"{tag} fwd wo", "nt", T, d, d, L),
+                  (f"{tag} fwd w13", "nt", T, 2 * f, d, L), (f"{tag} fwd w2", "nt", T, d, f, L),
+                  (f"{tag} fwd head", "nt", T, V, d, 1), (f"{tag} dX qkv", "nn", T, d, qkv, L),
+                  (f"{tag} dX wo", "nn", T, d, d, L), (f"{tag} dX w13", "nn", T, d, 2 * f, L),
+                  (f"{tag} dX w2", "nn", T, f, d, L), (f"{tag} dX head", "nn", T, d, V, 1),
+                  (f"{tag} dW qkv", "tn", qkv, d, T, L), (f"{tag} dW w13", "tn", 2 * f, d, T, L),
+                  (f"{tag} dW head", "tn", V, d, T, 1)]
 tot_h = tot_b = 0.0
 for name, kind, M, N, Kd, cnt in cases:
     fl = 2.0 * M * N * Kd

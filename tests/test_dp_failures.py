@@ -89,8 +89,7 @@ def _assert_same_state(a, b):
     for i in a["optimizer"]["state"]:
         for key in ("exp_avg", "exp_avg_sq", "step"):
             assert torch.equal(a["optimizer"]["state"][i][key], b["optimizer"]["state"][i][key]), (i, key)
-    assert a["lr_scheduler"]["last_epoch"] == b["lr_scheduler"]["last_epoch"]
-    assert a["lr_scheduler"]["_last_lr"] == b["lr_scheduler"]["_last_lr"]
+    assert a["lr_scheduler"] == b["lr_scheduler"]
     assert [s["next_step"] for s in a["data_loader"]] == [s["next_step"] for s in b["data_loader"]]
 
 

@@ -25,7 +25,9 @@ def rel(a, b):
 @pytest.mark.parametrize(
     "B,S,Hq,Hkv,D",
     [(1, 128, 2, 1, 128), (1, 256, 4, 2, 128), (2, 192, 4, 4, 64), (1, 2048, 32, 8, 128), (1, 320, 8, 2, 64),
-     (2, 512, 12, 12, 64)],
+     (2, 512, 12, 12, 64),
+     # long context (reduced heads) and sequence lengths that are not multiples of the 32/64/128 tiles
+     (1, 8192, 4, 1, 128), (1, 1000, 4, 2, 128), (2, 2047, 2, 1, 64), (1, 33, 2, 2, 128), (3, 100, 4, 4, 64)],
 )
 @pytest.mark.parametrize("mode", [0, 1])
 def test_flash_fwd_bwd(B, S, Hq, Hkv, D, mode):

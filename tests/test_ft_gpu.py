@@ -65,3 +65,56 @@ def test_gpu_sigusr1_saves_and_resubmits(tmp_path):
     assert calls and calls[0][-1] == "710", calls
     c = _load(d, 710)
     assert c["training_step"] >= 10
+
+
+def _same(a, b):
+    assert a["training_step"] == b["training_step"]
+    for k in a["model"]:
+        assert torch.equal(a["model"][k], b["model"][k]), k
+    for i in a["optimizer"]["state"]:
+        for key in ("exp_avg", "exp_avg_sq", "step"):
+            assert torch.equal(a["optimizer"]["state"][i][key], b["optimizer"]["state"][i][key]), (i, key)
+    assert a["lr_scheduler"] == b["lr_scheduler"]
+    assert a["data_loader"] == b["data_loader"]
+
+
+def test_gpu_async_periodic_checkpoint_equals_blocking_and_resumes_bit_exact(tmp_path):
+    """--save-every on the production path (HBM snapshot overlapping the next steps, pipelined
+    optimizer, dW side stream) writes the same bytes as a blocking save, and resumes bit-exactly."""
+    d = str(tmp_path)
+    write_fake_sbatch(d)
+    base = GPU + ["--checkpoint-path", os.path.join(d, "ck")]
+    rc, out = run_train(d, "720", base + ["--training-steps", "10", "--save-every", "4"], timeout=240)
+    assert rc == 0 and "Checkpoint written" in out, out[-3000:]
+    rc, out = run_train(d, "721", base + ["--training-steps", "10", "--save-every", "4", "--no-async-checkpoint"],
+                        timeout=240)
+    assert rc == 0, out[-3000:]
+    a, b = _load(d, 720), _load(d, 721)
+    assert a["training_step"] == 8  # the last periodic save (saves at 4 and 8)
+    _same(a, b)
+    rc, out = run_train(d, "722", base + ["--training-steps", "20", "--raise-error", "--error-step", "13",
+                                          "--checkpoint-id", "720"], timeout=240)
+    assert rc == 0 and "Resuming training from training_step 8" in out and "Checkpoint saved at step 13" in out
+    rc, out = run_train(d, "723", base + ["--training-steps", "20", "--raise-error", "--error-step", "13"],
+                        timeout=240)
+    assert rc == 0 and "Checkpoint saved at step 13" in out, out[-3000:]
+    _same(_load(d, 722), _load(d, 723))
+
+
+def test_gpu_nonfinite_gradient_saves_state_before_the_bad_step(tmp_path):
+    """Non-finite gradient norm (reference utils.py:61 error_if_nonfinite -> train.py:121-129): the
+    device-side sticky guard skips the update, the host finds the bad step two steps later and
+    rolls back to it; the file equals an injected-error save at that step."""
+    d = str(tmp_path)
+    write_fake_sbatch(d)
+    base = GPU[:-6] + ["--learning-rate", "1e30", "--lr-warmup-steps", "3", "--logging-frequency", "1",
+                       "--checkpoint-path", os.path.join(d, "ck"), "--training-steps", "30"]
+    rc, out = run_train(d, "730", base, timeout=240)
+    assert rc == 0 and "is non-finite at optimizer step" in out, out[-3000:]
+    import re
+
+    n = int(re.search(r"Checkpoint saved at step (\d+)", out).group(1))
+    assert 0 < n < 30
+    rc, out2 = run_train(d, "731", base + ["--raise-error", "--error-step", str(n)], timeout=240)
+    assert rc == 0 and f"Checkpoint saved at step {n}" in out2, out2[-3000:]
+    _same(_load(d, 730), _load(d, 731))
