@@ -33,6 +33,7 @@
 #include "torch_utils.h"
 
 #include <cstdlib>
+#include <string>
 #include <type_traits>
 #include <utility>
 
@@ -164,13 +165,15 @@ __device__ __forceinline__ void map_head(int hh, int Hq, int Hkv, int& h, int& k
 }
 
 // ================================================================== forward
-template <int D>
-__global__ __launch_bounds__(256, 2) void flash_fwd_kernel(const bf16_t* __restrict__ qk,
+// NW = waves per block (32 queries each): 4 by default; 2 when B * heads * query tiles is too
+// small to fill 256 CUs with 128-query blocks (GPT-2-sized models: 12-16 heads x 16 tiles).
+template <int D, int NW = 4>
+__global__ __launch_bounds__(64 * NW, 8 / NW) void flash_fwd_kernel(const bf16_t* __restrict__ qk,
                                                            const bf16_t* __restrict__ qkv,
                                                            bf16_t* __restrict__ out,
                                                            float* __restrict__ lse2, int B, int S,
                                                            int Hq, int Hkv, float sl2) {
-  constexpr int BM = 128, BN = 64, KS = D / 16, NDB = D / 32;
+  constexpr int BM = 32 * NW, BN = 64, KS = D / 16, NDB = D / 32;
   constexpr int TILE = BN * D * 2;
   // K | V tiles by LDS-DMA into two separate LDS objects, loop unrolled by two (as in the
   // dQ kernel): no staging VGPRs live across the tile's compute, no drained prefetch.
@@ -212,7 +215,7 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(const bf16_t* __restr
 
   const int kend = min((qt + 1) * BM, S);
   const int ntiles = (kend + BN - 1) / BN;
-  constexpr int GPW = TILE / 1024 / 4;  // glds instructions per wave per image
+  constexpr int GPW = TILE / 1024 / NW;  // glds instructions per wave per image
   auto dma = [&](int KT, auto BUF) {
     char* kb_ = decltype(BUF)::value ? kv1 : kv0;
     static_for<GPW>([&](auto I) {
@@ -621,12 +624,12 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_kernel(
 // wave per SIMD there is no other wave to fill the MFMA pipe during a softmax phase).
 // Q | dO pairs by LDS-DMA, double-buffered in two LDS objects (loop unrolled by two);
 // the slices' lse / delta ride along in LDS (registers are the scarce resource here).
-template <int D>
-__global__ __launch_bounds__(256, 1) void flash_bwd_dkdv2_kernel(
+template <int D, int NW = 4>
+__global__ __launch_bounds__(64 * NW, 4 / NW) void flash_bwd_dkdv2_kernel(
     const bf16_t* __restrict__ dO, const bf16_t* __restrict__ qk, const bf16_t* __restrict__ qkv,
     const float* __restrict__ lse2, const float* __restrict__ delta, bf16_t* __restrict__ dk_part,
     bf16_t* __restrict__ dv_part, int B, int S, int Hq, int Hkv, float sl2, float scale) {
-  constexpr int BK = 128, BQ = 32, KS = D / 16, NDB = D / 32;
+  constexpr int BK = 32 * NW, BQ = 32, KS = D / 16, NDB = D / 32;
   constexpr int QIMG = BQ * D * 2;          // one Q or dO slice
   constexpr int SLOT = 2 * QIMG + 256;      // Q | dO | lse[32] | delta[32] of one slice
   __shared__ __attribute__((aligned(16))) char pb0[2 * SLOT];  // pair buffer 0: slice A | slice B
@@ -664,7 +667,7 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkdv2_kernel(
   const int qs0 = kb0 / BQ;
   const int n = (S + BQ - 1) / BQ - qs0;  // slices of this key tile (>= 1)
   const int npairs = (n + 1) / 2;
-  constexpr int GPW = QIMG / 1024 / 4;    // glds instructions per wave per image
+  constexpr int GPW = QIMG / 1024 / NW;   // glds instructions per wave per image
   // pair p -> buffer: slices 2p (A) and 2p+1 (B, if any)
   auto dma = [&](int p, char* buf) __attribute__((always_inline)) {
 #pragma unroll
@@ -814,12 +817,12 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkdv2_kernel(
 // transposed LDS reads, B = dS^T straight from the accumulators). Every dQ element
 // is produced by exactly one wave in a fixed order: no atomics, bit-reproducible.
 // Used with flash_bwd_kernel<D, 1> (dK/dV only) for --deterministic runs.
-template <int D>
-__global__ __launch_bounds__(256, 1) void flash_bwd_dq_kernel(
+template <int D, int NW = 4>
+__global__ __launch_bounds__(64 * NW, 4 / NW) void flash_bwd_dq_kernel(
     const bf16_t* __restrict__ dO, const bf16_t* __restrict__ qk, const bf16_t* __restrict__ qkv,
     const float* __restrict__ lse2, const float* __restrict__ delta, bf16_t* __restrict__ dqkv, int B,
     int S, int Hq, int Hkv, float sl2, float scale) {
-  constexpr int BM = 128, BN = 64, KS = D / 16, NDB = D / 32;
+  constexpr int BM = 32 * NW, BN = 64, KS = D / 16, NDB = D / 32;
   constexpr int TILE = BN * D * 2;
   // K | V tiles arrive by LDS-DMA (no staging VGPRs held across the compute: at one wave
   // per SIMD the register-staged prefetch pushed the dQ accumulators through AGPR copies
@@ -859,7 +862,7 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dq_kernel(
 
   const int kend = min((qt + 1) * BM, S);
   const int ntiles = (kend + BN - 1) / BN;
-  constexpr int GPW = TILE / 1024 / 4;  // glds instructions per wave per image
+  constexpr int GPW = TILE / 1024 / NW;  // glds instructions per wave per image
   // tile KT -> buffer BUF: each lane moves one 16-B chunk; the swizzle is on the source
   auto dma = [&](int KT, auto BUF) {
     char* kb_ = decltype(BUF)::value ? kv1 : kv0;
@@ -1008,6 +1011,21 @@ bool g_dkdv2 = [] {
   return e == nullptr || std::atoi(e) != 0;
 }();
 
+// Waves (32 query or key rows each) per attention block: 2 when 4-wave blocks would leave
+// most of the 256 CUs idle (fewer than 512 blocks; head_dim 64 — the GPT-2-sized presets:
+// 12 / 16 heads x 16 tiles = 192 / 256 blocks at S = 2048), else 4.
+// The forward keeps 4-wave blocks (2 waves: 32.0 -> 36.6 us on GPT-2-small's layer); the
+// backward's dK/dV + dQ kernels gain (112.8 -> 94.2 us; 118.2 -> 99.2 us at 16 heads),
+// profiles/r2_flash_small_heads.log. FT_FLASH_NW=4 forces 4 (A/B).
+static const bool g_force_nw4 = [] {
+  const char* e = std::getenv("FT_FLASH_NW");
+  return e != nullptr && std::string(e) == "4";
+}();
+int waves_per_block(long S, long B, long Hq, long D) {
+  if (g_force_nw4) return 4;
+  return (D == 64 && ((S + 127) / 128) * B * Hq < 512) ? 2 : 4;
+}
+
 void check_inputs(const at::Tensor& qk, const at::Tensor& qkv, int64_t S, int64_t Hq, int64_t Hkv,
                   int64_t D) {
   FT_CHECK_CUDA(qk);
@@ -1036,8 +1054,9 @@ std::tuple<at::Tensor, at::Tensor> flash_fwd(const at::Tensor& qk, const at::Ten
   auto out = at::empty({T, Hq * D}, qk.options());
   auto lse = at::empty({B, Hq, (long)stat_stride(S)}, qk.options().dtype(at::kFloat));
   const float sl2 = LOG2E_F / std::sqrt((float)D);
-  const int nqt = (S + 127) / 128;
-  dim3 grid(nqt * B * Hq), block(256);
+  const int nw = 4;  // see waves_per_block
+  const int nqt = (S + 32 * nw - 1) / (32 * nw);
+  dim3 grid(nqt * B * Hq), block(64 * nw);
   if (D == 128)
     hipLaunchKernelGGL(flash_fwd_kernel<128>, grid, block, 0, ft_stream(), cptr<bf16_t>(qk),
                        cptr<bf16_t>(qkv), mptr<bf16_t>(out), mptr<float>(lse), B, (int)S, (int)Hq,
@@ -1078,32 +1097,36 @@ at::Tensor flash_bwd(const at::Tensor& dout, const at::Tensor& qk, const at::Ten
   const int pre_blocks = (int)((rows * 16 + 255) / 256);
   const int nkt = (S + 127) / 128;
   dim3 grid(nkt * B * Hq), block(256);
+  const int nw = waves_per_block(S, B, Hq, D);
+  const int nkt2 = (S + 32 * nw - 1) / (32 * nw);  // tiles of the deterministic dK/dV and dQ kernels
+  const dim3 grid2(nkt2 * B * Hq), block2(64 * nw);
   float* dqp = det ? nullptr : mptr<float>(dq_acc);
 #define FT_BWD(DD, MODE)                                                                          \
   hipLaunchKernelGGL((flash_bwd_kernel<DD, MODE>), grid, block, 0, ft_stream(), cptr<bf16_t>(dout), \
                      cptr<bf16_t>(qk), cptr<bf16_t>(qkv), cptr<float>(lse), cptr<float>(delta),     \
                      dqp, mptr<bf16_t>(dk_part), mptr<bf16_t>(dv_part), B, (int)S, (int)Hq, (int)Hkv, \
                      sl2, scale)
-#define FT_DKDV2(DD)                                                                               \
-  hipLaunchKernelGGL((flash_bwd_dkdv2_kernel<DD>), grid, block, 0, ft_stream(), cptr<bf16_t>(dout),    \
+#define FT_DKDV2(DD, NW_)                                                                          \
+  hipLaunchKernelGGL((flash_bwd_dkdv2_kernel<DD, NW_>), grid2, block2, 0, ft_stream(), cptr<bf16_t>(dout), \
                      cptr<bf16_t>(qk), cptr<bf16_t>(qkv), cptr<float>(lse), cptr<float>(delta),         \
                      mptr<bf16_t>(dk_part), mptr<bf16_t>(dv_part), B, (int)S, (int)Hq, (int)Hkv, sl2,    \
                      scale)
-#define FT_DQ(DD)                                                                                  \
-  hipLaunchKernelGGL((flash_bwd_dq_kernel<DD>), dim3(nkt * B * Hq), block, 0, ft_stream(),          \
+#define FT_DQ(DD, NW_)                                                                             \
+  hipLaunchKernelGGL((flash_bwd_dq_kernel<DD, NW_>), grid2, block2, 0, ft_stream(),                 \
                      cptr<bf16_t>(dout), cptr<bf16_t>(qk), cptr<bf16_t>(qkv), cptr<float>(lse),     \
                      cptr<float>(delta), mptr<bf16_t>(dqkv), B, (int)S, (int)Hq, (int)Hkv, sl2, scale)
   if (D == 128) {
     hipLaunchKernelGGL(flash_bwd_pre_kernel<128>, dim3(pre_blocks), block, 0, ft_stream(),
                        cptr<bf16_t>(dout), cptr<bf16_t>(out), mptr<float>(delta), B, (int)S, (int)Hq);
     if (mode == 0) FT_BWD(128, 0);
-    else if (mode == 1) { if (g_dkdv2) { FT_DKDV2(128); } else FT_BWD(128, 1); FT_DQ(128); }
+    else if (mode == 1) { if (g_dkdv2 && nw == 4) { FT_DKDV2(128, 4); } else FT_BWD(128, 1); FT_DQ(128, 4); }
     else FT_BWD(128, 2);
   } else {
     hipLaunchKernelGGL(flash_bwd_pre_kernel<64>, dim3(pre_blocks), block, 0, ft_stream(),
                        cptr<bf16_t>(dout), cptr<bf16_t>(out), mptr<float>(delta), B, (int)S, (int)Hq);
     if (mode == 0) FT_BWD(64, 0);
-    else if (mode == 1) { if (g_dkdv2) { FT_DKDV2(64); } else FT_BWD(64, 1); FT_DQ(64); }
+    else if (mode == 1 && nw == 2) { FT_DKDV2(64, 2); FT_DQ(64, 2); }
+    else if (mode == 1) { if (g_dkdv2) { FT_DKDV2(64, 4); } else FT_BWD(64, 1); FT_DQ(64, 4); }
     else FT_BWD(64, 2);
   }
 #undef FT_BWD

@@ -9,7 +9,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from fault_tolerant_llm_training_amd._native import kernels
 
 K = kernels()
-S, Hq, Hkv, D = 2048, 32, 8, 128
+# python scripts/flash_bench.py [S Hq Hkv D]  (default: the Llama-3-8B layer, S=2048, 32/8 heads, d=128)
+S, Hq, Hkv, D = (int(v) for v in sys.argv[1:5]) if len(sys.argv) >= 5 else (2048, 32, 8, 128)
+print(f"S={S} Hq={Hq} Hkv={Hkv} D={D}")
 qkv = torch.randn(S, (Hq + 2 * Hkv) * D, device="cuda").bfloat16()
 qk = torch.randn(S, (Hq + Hkv) * D, device="cuda").bfloat16()
 do = torch.randn(S, Hq * D, device="cuda").bfloat16()
