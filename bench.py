@@ -57,6 +57,9 @@ def parse():
     ap.add_argument("--no-ckpt", action="store_true", help="skip the checkpoint-save measurement")
     ap.add_argument("--grad-accum", type=int, default=1, help="micro-batches per optimizer step")
     ap.add_argument("--no-exposed-comm", action="store_true", help="skip the DP exposed-collective estimate")
+    ap.add_argument("--graph", action="store_true",
+                    help="1 GPU: replay each step as one HIP graph (optimizer of step k with forward/backward "
+                         "of step k+1): for launch-bound presets (gpt2-small / gpt2-medium)")
     ap.add_argument("--device", default="cuda")
     ap.add_argument("--dp-mode", default="", choices=["", "allreduce", "zero1"])
     ap.add_argument("--no-overlap", action="store_true", help="per-bucket optimizer as a serial phase (A/B)")
@@ -129,19 +132,41 @@ def main():
         sched.step()
         return loss
 
+    graphed = None
+    if a.graph:
+        if world > 1 or K > 1 or dev.type != "cuda":
+            raise SystemExit("--graph: one GPU, no gradient accumulation")
+        from fault_tolerant_llm_training_amd.graphs import GraphedStep
+
+        def fwd_bwd(tok, lab):
+            loss_ = model(tok, lab, inv_count)
+            loss_.backward()
+            red.finish()
+            return loss_
+
+        graphed = GraphedStep(model, red, opt, sched, fwd_bwd)
     for i in range(a.warmup):
-        loss = step(i)
+        if graphed is not None and i == a.warmup - 1:
+            loss = graphed.prime(*data.batch(i, B))  # eager fwd/bwd of step i, then capture
+        else:
+            loss = step(i)
     _sync(dev)
     fdist.barrier()
     _sync(dev)
     t0 = time.perf_counter()
     for i in range(a.steps):
-        loss = step(a.warmup + i)
+        if graphed is not None:  # optimizer of step i-1 + forward/backward of step i
+            loss = graphed.step(*data.batch(a.warmup + i, B))
+        else:
+            loss = step(a.warmup + i)
     opt.gate.wait_all()
     _sync(dev)
     fdist.barrier()
     _sync(dev)
     elapsed = time.perf_counter() - t0
+    if graphed is not None:
+        graphed.finish()  # the last backward's optimizer step (outside the timed window)
+        opt.graph_mode = False
     elapsed = fdist.ctrl_allreduce_max(int(elapsed * 1e9)) / 1e9
     # each rank's loss is its token sum over the GLOBAL token count: the global mean is the sum
     final_loss = fdist.ctrl_allreduce_sum(float(loss.item())) if world > 1 else float(loss.item())
@@ -184,6 +209,8 @@ def main():
         if red.sparse_embedding else 0.0,
         "recompute_layers": model.recompute_layers,
     }
+    if graphed is not None:
+        out["hip_graph"] = True
     if dev.type == "cuda":
         ms_ = torch.cuda.memory_stats(dev)
         out["hbm_peak_gb"] = round(ms_.get("reserved_bytes.all.peak", 0) / 2**30, 1)

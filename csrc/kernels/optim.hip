@@ -132,8 +132,17 @@ __global__ __launch_bounds__(256) void adamw_kernel(P* __restrict__ p, const P* 
                                                     long n8, float lr, float beta1, float beta2,
                                                     float eps, float wd, float inv_bc1,
                                                     float inv_sqrt_bc2,
-                                                    const float* __restrict__ stats) {
+                                                    const float* __restrict__ stats,
+                                                    const float* __restrict__ hyper) {
   if (stats[2] != 0.f) return;  // non-finite gradient norm: skip the whole update
+  if (hyper != nullptr) {
+    // [lr, 1/bc1, 1/sqrt(bc2)] from device memory: a HIP-graph replay of the optimizer reads
+    // this step's values (the host fills the buffer before the replay) instead of the
+    // scalars baked in at capture
+    lr = hyper[0];
+    inv_bc1 = hyper[1];
+    inv_sqrt_bc2 = hyper[2];
+  }
   const float coef = stats[1];
   const float decay = 1.f - lr * wd;
   const float step = lr * inv_bc1;
@@ -201,7 +210,13 @@ void grad_norm_(const at::Tensor& grad, const at::Tensor& stats, double max_norm
 
 void adamw_(const at::Tensor& p, const at::Tensor& g, const at::Tensor& m, const at::Tensor& v,
             const at::Tensor& stats, double lr, double beta1, double beta2, double eps, double wd,
-            int64_t step, int64_t max_blocks) {
+            int64_t step, int64_t max_blocks, const std::optional<at::Tensor>& hyper) {
+  const float* hp = nullptr;
+  if (hyper.has_value() && hyper->defined()) {
+    FT_CHECK_F32((*hyper));
+    TORCH_CHECK(hyper->is_cuda() && hyper->numel() >= 3, "adamw: hyper must be a device fp32[3]");
+    hp = cptr<float>(*hyper);
+  }
   FT_CHECK_CUDA(p);
   FT_CHECK_CONTIG(p);
   FT_CHECK_CONTIG(g);
@@ -230,11 +245,11 @@ void adamw_(const at::Tensor& p, const at::Tensor& g, const at::Tensor& m, const
   if (nt)                                                                                           \
     hipLaunchKernelGGL((adamw_kernel<PT, ST, true>), grid, block, 0, ft_stream(), mptr<PT>(p),       \
                        cptr<PT>(g), mptr<ST>(m), mptr<ST>(v), n8, (float)lr, (float)beta1,          \
-                       (float)beta2, (float)eps, (float)wd, inv_bc1, inv_sqrt_bc2, cptr<float>(stats)); \
+                       (float)beta2, (float)eps, (float)wd, inv_bc1, inv_sqrt_bc2, cptr<float>(stats), hp); \
   else                                                                                              \
     hipLaunchKernelGGL((adamw_kernel<PT, ST, false>), grid, block, 0, ft_stream(), mptr<PT>(p),      \
                        cptr<PT>(g), mptr<ST>(m), mptr<ST>(v), n8, (float)lr, (float)beta1,          \
-                       (float)beta2, (float)eps, (float)wd, inv_bc1, inv_sqrt_bc2, cptr<float>(stats)); \
+                       (float)beta2, (float)eps, (float)wd, inv_bc1, inv_sqrt_bc2, cptr<float>(stats), hp); \
   } while (0)
   if (p.scalar_type() == at::kBFloat16 && m.scalar_type() == at::kBFloat16) FT_ADAM(bf16_t, bf16_t);
   else if (p.scalar_type() == at::kBFloat16 && m.scalar_type() == at::kFloat) FT_ADAM(bf16_t, float);
@@ -278,6 +293,6 @@ TORCH_LIBRARY_FRAGMENT(ftamd, m) {
   m.def("grad_norm_(Tensor grad, Tensor(a!) stats, float max_norm) -> ()", &grad_norm_);
   m.def(
       "adamw_(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, Tensor stats, float lr, float "
-      "beta1, float beta2, float eps, float wd, int step, int max_blocks=0) -> ()",
+      "beta1, float beta2, float eps, float wd, int step, int max_blocks=0, Tensor? hyper=None) -> ()",
       &adamw_);
 }

@@ -116,6 +116,12 @@ class FlatAdamW(torch.optim.Optimizer):
         self._stats_event = None
         self._stats_step = -1
         self.gate = ParamGate()
+        # HIP-graph mode (graphs.GraphedStep): lr and bias corrections come from this device
+        # buffer, filled from a ring of pinned host slots before each replay
+        self.graph_mode = False
+        self.hyper = torch.zeros(3, dtype=torch.float32, device=flat.device)
+        self._hyper_ring = [torch.zeros(3, dtype=torch.float32, pin_memory=self._pin) for _ in range(16)]
+        self._hyper_i = 0
         # grid cap for the per-bucket AdamW launches that run concurrently with the next
         # forward's GEMMs (fewer blocks = less contention for CU issue slots)
         self.overlap_blocks = int(os.environ.get("FT_ADAMW_BLOCKS", "0"))
@@ -144,9 +150,26 @@ class FlatAdamW(torch.optim.Optimizer):
         b1, b2 = grp["betas"]
         return float(grp["lr"]), b1, b2, grp["eps"], grp["weight_decay"]
 
+    def stage_hyper(self, step: int) -> None:
+        """Graph mode: enqueue the H2D copy of [lr, 1/bc1, 1/sqrt(bc2)] of optimizer step
+        ``step`` into ``self.hyper`` (on the current stream, ahead of the replay that uses it),
+        rounded to fp32 exactly like the host path of adamw_ (optim.hip): bc = 1.f - (float)beta^step,
+        then 1/bc and 1/sqrtf(bc) in float."""
+        import numpy as np
+
+        lr, b1, b2, _eps, _wd = self._hyper()
+        bc1 = np.float32(1.0) - np.float32(b1 ** step)  # 1.f - (float)std::pow(beta, step)
+        bc2 = np.float32(1.0) - np.float32(b2 ** step)
+        h = self._hyper_ring[self._hyper_i % len(self._hyper_ring)]
+        self._hyper_i += 1
+        h.copy_(torch.from_numpy(np.array([np.float32(lr), np.float32(1.0) / bc1,
+                                           np.float32(1.0) / np.sqrt(bc2)], dtype=np.float32)))
+        self.hyper.copy_(h, non_blocking=True)
+
     def _update(self, p, g, m, v, lr, b1, b2, eps, wd, max_blocks: int = 0):
         if p.is_cuda:
-            kernels().adamw_(p, g, m, v, self.stats, lr, b1, b2, eps, wd, self.step_count, max_blocks)
+            kernels().adamw_(p, g, m, v, self.stats, lr, b1, b2, eps, wd, self.step_count, max_blocks,
+                             self.hyper if self.graph_mode else None)
         else:
             _adamw_reference(p, g, m, v, self.stats, lr, b1, b2, eps, wd, self.step_count)
 
@@ -177,7 +200,8 @@ class FlatAdamW(torch.optim.Optimizer):
                 kernels().norm_finish_(total, self.stats, self.max_grad_norm)
             else:
                 _norm_reference(total.sum().reshape(1), self.stats, self.max_grad_norm)
-            self._publish_stats()
+            if not self.graph_mode:  # graph replays publish after the replay (publish_stats)
+                self._publish_stats()
             for b in sorted(r.buckets, key=lambda b: b.lo):  # forward order
                 slo, shi = r.state_range(b)
                 self._update(r.param_for_update(b), r.grad_for_update(b), self.exp_avg[slo:shi],
@@ -211,6 +235,10 @@ class FlatAdamW(torch.optim.Optimizer):
             h.copy_(self.stats)
         self._ring_steps[i] = self.step_count
         self._stats_step = self.step_count
+
+    def publish_stats(self) -> None:
+        """Graph mode: copy the stats of the step the last replay ran to the host ring."""
+        self._publish_stats()
 
     def norm_for_logging(self):
         """(device tensor holding the last step's pre-clip grad norm, event after which it is valid)."""

@@ -142,6 +142,10 @@ class _StopTraining(Exception):
         self.cause = cause
 
 
+class _GraphDone(Exception):
+    """Internal: the step ran as a graph replay (skips the eager compute block)."""
+
+
 class _FatalStepError(Exception):
     """A failure left this rank unable to finish its share of the step's collectives."""
 
@@ -426,6 +430,7 @@ def train(args) -> int:
         if not (sig_all or err_all or bad_all):
             return
         # stop: every rank reached the same decision from the same table
+        complete_pending()  # graph mode: the last backward's optimizer step first
         rolled = rollback_to_first_bad()
         if sig_all == SIGTERM_NUM:
             raise _StopTraining(SignalInterrupt(sig_all))
@@ -442,6 +447,30 @@ def train(args) -> int:
     boundary.count_sum = 0.0
     emb_dim = margs.dim
     exit_code = 0
+
+    graphed = None
+    if args.hip_graph:
+        if info.distributed or K > 1 or device.type != "cuda":
+            raise ValueError("--hip-graph: one GPU without a process group, --grad-accum 1, --device cuda")
+        from .graphs import GraphedStep
+
+        inv_dev = torch.empty(1, dtype=torch.float32, device=device)  # static input of the graph
+
+        def _fwd_bwd(tok_, lab_):
+            l_ = model(tok_, lab_, inv_dev)
+            l_.backward()
+            reducer.finish()
+            return l_
+
+        graphed = GraphedStep(model, reducer, optimizer, lr_scheduler, _fwd_bwd)
+        logger.info("HIP graph: each step replays [optimizer(k) | forward+backward(k+1)] as one graph")
+
+    def complete_pending():
+        """Graph mode: run the last backward's optimizer step (before a checkpoint / at the end)."""
+        if graphed is not None and graphed.pending:
+            if ckpt["engine"] is not None:
+                ckpt["engine"].fence()
+            graphed.finish()
 
     try:
         while training_step < args.training_steps:
@@ -481,11 +510,25 @@ def train(args) -> int:
             else:
                 c = torch.tensor([max(1.0, boundary.count_sum)], dtype=torch.float64).reciprocal_().float()
                 inv = c.to(device, non_blocking=True)
-            tok_all = batch.inputs.to(device, non_blocking=True)
-            lab_all = batch.labels.to(device, non_blocking=True)
-            phase = "forward"
-            loss = None
+            if graphed is not None:
+                inv_dev.copy_(inv, non_blocking=True)
+                lr_now = optimizer.param_groups[0]["lr"]
+                if graphed.ready:
+                    if ckpt["engine"] is not None:
+                        ckpt["engine"].fence()  # the replay's optimizer must follow a pending snapshot
+                    loss = graphed.step(batch.inputs, batch.labels)  # optimizer(k-1) + fwd/bwd(k)
+                else:
+                    loss = graphed.prime(batch.inputs, batch.labels)  # eager fwd/bwd(k), capture
+                loss = loss.detach().clone()
+                phase = "graph"
+            tok_all = batch.inputs.to(device, non_blocking=True) if graphed is None else None
+            lab_all = batch.labels.to(device, non_blocking=True) if graphed is None else None
+            phase = "forward" if graphed is None else "graph"
+            if graphed is None:
+                loss = None
             try:
+                if graphed is not None:
+                    raise _GraphDone()
                 for k in range(K):
                     reducer.begin_micro(k, K)
                     tok, lab = tok_all[k * B : (k + 1) * B], lab_all[k * B : (k + 1) * B]
@@ -511,6 +554,8 @@ def train(args) -> int:
                 lr_scheduler.step()
                 phase = "post"
                 fault.fire(training_step, "post")
+            except _GraphDone:
+                pass
             except Exception as e:  # noqa: BLE001
                 logger.error(f"Training error at step {training_step} ({phase}): {e!r}")
                 pending_err = e
@@ -545,7 +590,9 @@ def train(args) -> int:
                 prof, prof_range = None, None
             if (pending_err is None and args.save_every and training_step % args.save_every == 0
                     and training_step < args.training_steps):
+                complete_pending()  # graph mode: the snapshot needs this step's optimizer update
                 save_checkpoint(blocking=args.no_async_checkpoint, step_now=training_step)
+        complete_pending()
         boundary.count = 0.0
         boundary(final=True)  # drains the loss log, last non-finite check, last signals
         if ckpt["engine"] is not None:
