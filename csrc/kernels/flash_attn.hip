@@ -1010,6 +1010,10 @@ bool g_dkdv2 = [] {
   const char* e = std::getenv("FT_FLASH_DKDV2");
   return e == nullptr || std::atoi(e) != 0;
 }();
+bool g_dkdv2_64 = [] {
+  const char* e = std::getenv("FT_FLASH_DKDV2");
+  return e != nullptr && std::atoi(e) == 2;
+}();
 
 // Waves (32 query or key rows each) per attention block: 2 when 4-wave blocks would leave
 // most of the 256 CUs idle (fewer than 512 blocks; head_dim 64 — the GPT-2-sized presets:
@@ -1126,7 +1130,9 @@ at::Tensor flash_bwd(const at::Tensor& dout, const at::Tensor& qk, const at::Ten
                        cptr<bf16_t>(dout), cptr<bf16_t>(out), mptr<float>(delta), B, (int)S, (int)Hq);
     if (mode == 0) FT_BWD(64, 0);
     else if (mode == 1 && nw == 2) { FT_DKDV2(64, 2); FT_DQ(64, 2); }
-    else if (mode == 1) { if (g_dkdv2) { FT_DKDV2(64, 4); } else FT_BWD(64, 1); FT_DQ(64, 4); }
+    // head_dim 64 with 4-wave blocks: the one-slice dK/dV kernel is faster (S = 8192, 16 heads:
+    // 631 vs 783 us, profiles/r2_flash_long_context.log); FT_FLASH_DKDV2=2 forces the slice pair
+    else if (mode == 1) { if (g_dkdv2_64) { FT_DKDV2(64, 4); } else FT_BWD(64, 1); FT_DQ(64, 4); }
     else FT_BWD(64, 2);
   }
 #undef FT_BWD
