@@ -235,7 +235,7 @@ def main():
         dry = fdist.ctrl_allreduce_max(int(dry * 1e6)) / 1e6
         out["compute_only_ms_per_step"] = round(dry, 2)
         out["exposed_comm_ms_per_step"] = round(ms - dry, 2)
-    if not a.no_ckpt and dev.type == "cuda":
+    if not a.no_ckpt:
         import tempfile
 
         from fault_tolerant_llm_training_amd.ckpt.bench_save import measure_checkpoint

@@ -15,6 +15,12 @@ are measured here, both through the same engine the trainer uses
   (``visible_s``): snapshot enqueue on the host, the compute stream's wait for
   the HBM snapshot before the next optimizer step, and the snapshot/drain DMA
   contending with the GEMMs for HBM.
+
+Under data parallelism every step runs collectives, so every rank must run the
+same number of steps: the "file durable" test that ends the loaded phase is a
+rank-local poll, agreed on after each step over the gloo control group (the save
+counts as done once every rank's share is durable). On the CPU (gloo tests) the
+step times are host clock stamps after each step instead of device events.
 """
 from __future__ import annotations
 
@@ -44,6 +50,12 @@ def measure_checkpoint(model, optimizer, lr_scheduler, step_fn, first_step: int,
     from ..parallel import dist as fdist
 
     dev = model.flat.device
+    cuda = dev.type == "cuda"
+
+    def sync():
+        if cuda:
+            torch.cuda.synchronize(dev)
+
     eng = _engine(model, optimizer, info, mode)
     t0 = time.perf_counter()
     eng.preallocate()
@@ -55,7 +67,7 @@ def measure_checkpoint(model, optimizer, lr_scheduler, step_fn, first_step: int,
 
     # ---- exit-path save: the training loop is stopped until the file is durable
     optimizer.gate.wait_all()
-    torch.cuda.synchronize(dev)
+    sync()
     fdist.barrier()
     t0 = time.perf_counter()
     st = eng.save(path, build, blocking=True)
@@ -72,21 +84,34 @@ def measure_checkpoint(model, optimizer, lr_scheduler, step_fn, first_step: int,
     i = first_step
     evs = []
 
+    def stamp():
+        if cuda:
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+            return ev
+        return time.perf_counter()
+
+    def elapsed_ms(a, b):
+        return a.elapsed_time(b) if cuda else (b - a) * 1e3
+
     def run(n_or_until):
         nonlocal i
         k = 0
         while True:
             step_fn(i, eng.fence)
-            ev = torch.cuda.Event(enable_timing=True)
-            ev.record()
-            evs.append(ev)
+            evs.append(stamp())
             i += 1
             k += 1
             if isinstance(n_or_until, int):
                 if k >= n_or_until:
                     return k
-            elif n_or_until() or k >= max_loaded_steps:
-                return k
+            else:
+                # one decision for every rank (each step runs collectives)
+                stop = n_or_until() or k >= max_loaded_steps
+                if info.world_size > 1:
+                    stop = fdist.ctrl_allreduce_sum(1.0 if stop else 0.0) >= info.world_size
+                if stop:
+                    return k
 
     run(1)
     run(steady_steps)
@@ -108,8 +133,8 @@ def measure_checkpoint(model, optimizer, lr_scheduler, step_fn, first_step: int,
         return done["k"] >= 2  # two steady steps after the file is durable
 
     run(finished)
-    torch.cuda.synchronize(dev)
-    dts = [evs[j - 1].elapsed_time(evs[j]) for j in range(1, len(evs))]
+    sync()
+    dts = [elapsed_ms(evs[j - 1], evs[j]) for j in range(1, len(evs))]
     steady = dts[: n_steady - 1]
     loaded = dts[n_steady - 1:]
     med = statistics.median(steady)

@@ -28,9 +28,11 @@ def _port():
     return p
 
 
-def _env():
+def _env(ckpt_dir=None):
     env = dict(os.environ)
     env["OMP_NUM_THREADS"] = "1"
+    if ckpt_dir is not None:
+        env["FT_BENCH_CKPT_DIR"] = str(ckpt_dir)
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
         env.pop(k, None)
     return env
@@ -40,9 +42,18 @@ def _json_lines(out):
     return [json.loads(ln) for ln in out.splitlines() if ln.startswith("{")]
 
 
-def test_bench_single_process_json():
-    r = subprocess.run([sys.executable, "bench.py"] + ARGS, cwd=ROOT, env=_env(), capture_output=True, text=True,
-                       timeout=300)
+def _check_ckpt(j, world):
+    """The checkpoint-save block (second half of the BASELINE metric) ran without error; under DP
+    every rank ran the same loaded steps (a mismatch would have hung the collectives)."""
+    c = j["ckpt_save"]
+    assert "error" not in c, c
+    assert c["exit_save_s"] > 0 and c["bytes"] > 0
+    assert c["loaded"]["steps_until_durable"] >= 3 and c["loaded"]["save_to_durable_s"] is not None
+
+
+def test_bench_single_process_json(tmp_path):
+    r = subprocess.run([sys.executable, "bench.py"] + ARGS, cwd=ROOT, env=_env(tmp_path), capture_output=True,
+                       text=True, timeout=300)
     assert r.returncode == 0, r.stderr
     lines = _json_lines(r.stdout)
     assert len(lines) == 1
@@ -52,13 +63,14 @@ def test_bench_single_process_json():
         assert k in j, k
     assert j["n_gpus"] == 1 and j["steps"] == 2 and j["config"]["parallelism"] == "dp1"
     assert abs(j["value"] - 64 / (j["ms_per_step"] / 1e3)) / j["value"] < 0.02
+    _check_ckpt(j, 1)
 
 
 @pytest.mark.parametrize("mode", ["zero1", "allreduce"])
-def test_bench_torchrun_two_ranks(mode):
+def test_bench_torchrun_two_ranks(mode, tmp_path):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
            "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2", "--dp-mode", mode] + ARGS
-    r = subprocess.run(cmd, cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=300)
+    r = subprocess.run(cmd, cwd=ROOT, env=_env(tmp_path), capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = _json_lines(r.stdout)
     assert len(lines) == 1, r.stdout  # rank 0 only
@@ -69,11 +81,12 @@ def test_bench_torchrun_two_ranks(mode):
     # vs_baseline is per GPU (the metric is tokens/sec/GPU): it does not scale with N by itself
     assert abs(j["vs_baseline"] - j["tokens_per_s_per_gpu"] / 6376.0) < 1e-3
     assert "exposed_comm_ms_per_step" in j and "compute_only_ms_per_step" in j
+    _check_ckpt(j, 2)
 
 
-def test_bench_grad_accum_two_ranks():
+def test_bench_grad_accum_two_ranks():  # (no checkpoint block: --no-ckpt)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
-           "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2", "--grad-accum", "2"] + ARGS
+           "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2", "--grad-accum", "2", "--no-ckpt"] + ARGS
     r = subprocess.run(cmd, cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     j = _json_lines(r.stdout)[0]
