@@ -55,6 +55,9 @@ def parse():
     ap.add_argument("--ckpt-dir", default="", help="directory for the checkpoint-save measurement "
                     "(default: $FT_BENCH_CKPT_DIR or <tmpdir>/ft_bench_ckpt)")
     ap.add_argument("--no-ckpt", action="store_true", help="skip the checkpoint-save measurement")
+    ap.add_argument("--ckpt-mode", default="auto", choices=["auto", "hbm", "host"],
+                    help="checkpoint snapshot: 'hbm' (D2D into spare HBM, then drained to host), 'host' "
+                         "(straight to pinned host memory), 'auto' (hbm when the free HBM holds it)")
     ap.add_argument("--grad-accum", type=int, default=1, help="micro-batches per optimizer step")
     ap.add_argument("--no-exposed-comm", action="store_true", help="skip the DP exposed-collective estimate")
     ap.add_argument("--graph", action="store_true",
@@ -242,7 +245,7 @@ def main():
 
         d = a.ckpt_dir or os.environ.get("FT_BENCH_CKPT_DIR") or os.path.join(tempfile.gettempdir(), "ft_bench_ckpt")
         try:
-            out["ckpt_save"] = measure_checkpoint(model, opt, sched, step, nxt, d, info)
+            out["ckpt_save"] = measure_checkpoint(model, opt, sched, step, nxt, d, info, mode=a.ckpt_mode)
         except Exception as e:  # noqa: BLE001 - keep the throughput line; report why the save failed
             out["ckpt_save"] = {"error": repr(e)[:300], "dir": d}
     if info.is_main:

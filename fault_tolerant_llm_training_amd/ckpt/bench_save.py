@@ -147,6 +147,7 @@ def measure_checkpoint(model, optimizer, lr_scheduler, step_fn, first_step: int,
     return {
         "bytes": st.bytes,
         "mode": eng.mode,
+        "hbm_in_use_gb_at_save": round(torch.cuda.memory_reserved(dev) / 2**30, 1) if cuda else None,
         "pinned_alloc_s": round(alloc_s, 3),
         "exit_save_s": round(exit_s, 3),
         "exit_save_GB_per_s": round(st.bytes / exit_s / 1e9, 2),
