@@ -1,5 +1,5 @@
 #!/bin/bash
-# Checkpoint save vs HBM footprint (BASELINE config 5): writer throughput of the box's disk, then the 8B
+# Checkpoint save vs HBM footprint (BASELINE config 5), run on the GPU box: writer throughput of the box's disk, then the 8B
 # save in both snapshot modes at seq 2048 (~71 GB in use) and seq 32768 with block recompute (~105 GB).
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; L=gpurun_out/ckpt_footprint.log; rm -f $L
 df -T /tmp >> $L 2>&1
