@@ -1,0 +1,19 @@
+"""One GEMM shape, hand kernel and hipBLASLt, for rocprofv3 --pmc passes (scripts/gpu_pmc.sh).
+    python scripts/gemm_pmc_probe.py [M N K]   (default: the 8B w13 forward, 2048 x 28672 x 4096)
+"""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from fault_tolerant_llm_training_amd._native import kernels  # noqa: E402
+
+M, N, K = (int(v) for v in sys.argv[1:4]) if len(sys.argv) >= 4 else (2048, 28672, 4096)
+a = (torch.rand(M, K, device="cuda") * 2 - 1).bfloat16()
+b = (torch.rand(N, K, device="cuda") * 2 - 1).bfloat16()
+k = kernels()
+for _ in range(20):
+    k.gemm(a, True, b, True, M, N, K, None, None, False, 1)
+    torch.mm(a, b.t())
+torch.cuda.synchronize()
