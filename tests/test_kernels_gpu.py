@@ -317,16 +317,19 @@ def test_pinned_ring_h2d():
     release()
 
 
-@pytest.mark.parametrize("T,F_", [(64, 64), (192, 320), (512, 1408)])
+@pytest.mark.parametrize("T,F_", [(64, 64), (192, 320), (512, 1408), (256, 14336)])
 def test_swiglu_transposed_outputs(K, T, F_):
     """Tiled SwiGLU kernels: the row-major outputs equal the elementwise kernels' bitwise,
-    and the extra transposed outputs are exact transposes."""
+    and the extra transposed outputs are exact transposes (plain=False writes only the
+    transpose)."""
     gu = torch.randn(T, 2 * F_, device="cuda").bfloat16()
     a, aT = K.swiglu_fwd_t(gu)
     assert torch.equal(a, K.swiglu_fwd(gu)) and torch.equal(aT, a.t().contiguous())
     da = torch.randn(T, F_, device="cuda").bfloat16()
     dgu, dguT = K.swiglu_bwd_t(da, gu)
+    empty, dguT2 = K.swiglu_bwd_t(da, gu, False)
     assert torch.equal(dgu, K.swiglu_bwd(da, gu)) and torch.equal(dguT, dgu.t().contiguous())
+    assert empty.numel() == 0 and torch.equal(dguT2, dguT)
 
 
 @pytest.mark.parametrize("mode,t_only", [("all", False), ("all", True), ("none", False)])
