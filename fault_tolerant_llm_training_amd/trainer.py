@@ -247,6 +247,8 @@ def train(args) -> int:
     if loader_state is not None and int(loader_state.get("next_step", start_step)) != start_step:
         raise ValueError("data-loader state does not match training_step in the checkpoint")
     loader = TrainLoader(source, start_step=start_step, state=loader_state, prefetch=args.prefetch)
+    if loader_state is not None:
+        logger.info(f"Data loader position restored: {loader_state}")
 
     logger.info("Setting up Model...")
     margs = model_args_for(args.model, vocab_size=holder["vocab"], seq_len=args.sequence_length)
