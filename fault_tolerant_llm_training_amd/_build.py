@@ -29,7 +29,7 @@ PKG = Path(__file__).resolve().parent
 ROOT = PKG.parent
 CSRC = ROOT / "csrc"
 BUILD = ROOT / "build"
-ARCH = os.environ.get("FT_OFFLOAD_ARCH", "gfx950")
+ARCH = "gfx950"  # MI355X (CDNA4) only
 
 KERNELS_SO = PKG / "_kernels.so"
 RUNTIME_SO = PKG / "_runtime.so"
