@@ -68,6 +68,8 @@ def parse():
     ap.add_argument("--no-overlap", action="store_true", help="per-bucket optimizer as a serial phase (A/B)")
     ap.add_argument("--activation-checkpointing", type=int, default=0,
                     help="recompute this many blocks in backward (-1 = all): long-context runs")
+    ap.add_argument("--recompute-attention", action="store_true",
+                    help="with --activation-checkpointing: re-run flash fwd too (default keeps its output)")
     ap.add_argument("--whole-buffer-optimizer", action="store_true",
                     help="1 GPU: one norm + one AdamW launch over the flat buffer after backward (A/B)")
     return ap.parse_args()
@@ -100,7 +102,7 @@ def main():
     margs = model_args_for(a.model, vocab_size=a.vocab_size, seq_len=a.seq_len)
     model = build_model(margs, dev, torch.bfloat16, seed=1234)
     if a.activation_checkpointing:
-        model.set_activation_checkpointing(a.activation_checkpointing)
+        model.set_activation_checkpointing(a.activation_checkpointing, recompute_attention=a.recompute_attention)
     red = GradReducer(model.flat, model.sinks_in_backward_order(), bucket_mb=a.bucket_mb,
                       mode=a.dp_mode or None, overlap=not a.no_overlap)
     if a.whole_buffer_optimizer and world == 1:

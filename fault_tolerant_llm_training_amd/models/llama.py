@@ -130,11 +130,14 @@ class TransformerBlock(nn.Module):
         self.ffn_norm = _Weight(a.dim)
         self.eps = a.norm_eps
         self.layernorm = a.norm_type == "layernorm"
+        self.attn_keep = Fx.AttentionKeep()
 
-    def forward(self, h, d, cos, sin, seq_len):
+    def forward(self, h, d, cos, sin, seq_len, gen=None):
         """Pre-norm block (reference model.py:310-311) on the residual stream ``h`` with the
         previous block's pending output ``d`` (its add is fused into this block's first norm).
-        Returns (h', d') with the block output h' + d' still to be added."""
+        Returns (h', d') with the block output h' + d' still to be added. ``gen``: the model's
+        forward generation when this block is recomputed in backward with its attention output
+        kept (selective checkpointing); None otherwise."""
         at, ff = self.attention, self.feed_forward
         sk = lambda p: getattr(p, "_ft_sink", None)  # noqa: E731
         if d is None:
@@ -143,7 +146,8 @@ class TransformerBlock(nn.Module):
             h, xn = Fx.add_norm(h, d, self.attention_norm.weight, sk(self.attention_norm.weight), self.eps,
                                 self.layernorm)
         qkv = Fx.linear(xn, at.wqkv, at.wqkv_sink)
-        o = Fx.rope_attention(qkv.view(-1, qkv.shape[-1]), cos, sin, seq_len, at.n_heads, at.n_kv_heads, at.head_dim)
+        o = Fx.rope_attention(qkv.view(-1, qkv.shape[-1]), cos, sin, seq_len, at.n_heads, at.n_kv_heads, at.head_dim,
+                              self.attn_keep if gen is not None else None, -1 if gen is None else gen)
         da = Fx.linear(o.view(*h.shape[:-1], -1), at.wo.weight, sk(at.wo.weight))
         h, hn = Fx.add_norm(h, da, self.ffn_norm.weight, sk(self.ffn_norm.weight), self.eps, self.layernorm)
         return h, Fx.feed_forward(hn, ff.w13, ff.w2.weight, ff.w13_sink, sk(ff.w2.weight))
@@ -167,13 +171,19 @@ class Transformer(nn.Module):
         self.gate = None  # optim.adamw.ParamGate: per-layer wait for the optimizer's updates
         self._ranges = None
         self.recompute_layers = 0  # activation checkpointing: blocks [0, n) recompute in backward
+        self.recompute_attention = False  # False: recomputed blocks keep their attention output
+        self._gen = 0  # forward generation (tags kept attention outputs)
 
-    def set_activation_checkpointing(self, n_layers: int) -> None:
+    def set_activation_checkpointing(self, n_layers: int, recompute_attention: bool = False) -> None:
         """Recompute the first ``n_layers`` blocks (-1: all) during backward instead of keeping
-        their activations: only each block's input residual stream stays resident. Costs one
-        extra block forward; extends the reachable sequence length / batch per GPU (SURVEY.md
-        §5.7 — the reference relies on SDPA's O(S) attention memory alone, model.py:212)."""
+        their activations: each block's input residual stream and — unless
+        ``recompute_attention`` — its attention output and log-sum-exp stay resident, so the
+        recompute runs the norms, projections, RoPE and FFN but not the flash forward (the
+        O(S^2) part; T x Hq x D bf16 per block, 0.5 GB at seq 65536 for Llama-3-8B).
+        Extends the reachable sequence length / batch per GPU (SURVEY.md §5.7 — the reference
+        relies on SDPA's O(S) attention memory alone, model.py:212)."""
         self.recompute_layers = self.n_layers if n_layers < 0 else min(int(n_layers), self.n_layers)
+        self.recompute_attention = bool(recompute_attention)
 
     # ------------------------------------------------------------------ materialisation
     def flat_layout(self):
@@ -262,12 +272,15 @@ class Transformer(nn.Module):
         h = Fx.embedding(tokens, self.tok_embeddings.weight, sk(self.tok_embeddings.weight))
         cos, sin = self.rope_cos, self.rope_sin
         d = None
+        self._gen += 1
+        gen = None if self.recompute_attention else self._gen
         for i, layer in enumerate(self.layers.values()):
             self._wait(layer_r[i])
             if i < self.recompute_layers and torch.is_grad_enabled():
                 # non-reentrant: the custom Functions' saved tensors are dropped and regenerated
-                # by re-running the block (deterministic kernels → bit-identical gradients)
-                h, d = torch.utils.checkpoint.checkpoint(layer, h, d, cos, sin, S, use_reentrant=False)
+                # by re-running the block (deterministic kernels → bit-identical gradients);
+                # with ``gen`` the re-run reuses the kept attention output
+                h, d = torch.utils.checkpoint.checkpoint(layer, h, d, cos, sin, S, gen, use_reentrant=False)
             else:
                 h, d = layer(h, d, cos, sin, S)
         self._wait(final_r)

@@ -438,20 +438,47 @@ def attention_reference(qkv, cos, sin, seq_len, hq, hkv, d):
     return o.transpose(1, 2).reshape(T, hq * d)
 
 
+class AttentionKeep:
+    """Per-block holder of the attention output kept across a recomputed block (selective
+    activation checkpointing): the first forward of a checkpointed block stores (o, lse) here
+    tagged with the model's forward generation; the recompute in backward (same generation)
+    reuses them instead of running the flash forward again. A stale entry (a forward whose
+    backward never ran) carries an older generation and is simply overwritten."""
+
+    __slots__ = ("gen", "o", "lse")
+
+    def __init__(self):
+        self.gen, self.o, self.lse = -1, None, None
+
+
 class RopeAttentionFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, qkv, cos, sin, seq_len, hq, hkv, d):
+    def forward(ctx, qkv, cos, sin, seq_len, hq, hkv, d, keep=None, gen=-1):
         ctx.cfg = (seq_len, hq, hkv, d)
+        hit = keep is not None and keep.gen == gen and keep.o is not None
         if qkv.is_cuda:
             from .attention import flash_attn_fwd
 
             qkv = qkv.contiguous()
             qk = kernels().rope_fwd(qkv, cos, sin, seq_len, hq, hkv, d)
-            o, lse = flash_attn_fwd(qk, qkv, seq_len, hq, hkv, d)
+            if hit:  # recompute pass of a checkpointed block: the kept output (bit-identical)
+                o, lse = keep.o, keep.lse
+                keep.o = keep.lse = None
+            else:
+                o, lse = flash_attn_fwd(qk, qkv, seq_len, hq, hkv, d)
+                if keep is not None:
+                    keep.gen, keep.o, keep.lse = gen, o, lse
             ctx.save_for_backward(qkv, qk, o, lse, cos, sin)
             return o
         ctx.save_for_backward(qkv, cos, sin)
-        return attention_reference(qkv, cos, sin, seq_len, hq, hkv, d)
+        if hit:
+            o = keep.o
+            keep.o = None
+        else:
+            o = attention_reference(qkv, cos, sin, seq_len, hq, hkv, d)
+            if keep is not None:
+                keep.gen, keep.o = gen, o
+        return o
 
     @staticmethod
     def backward(ctx, do):
@@ -462,17 +489,19 @@ class RopeAttentionFn(torch.autograd.Function):
             qkv, qk, o, lse, cos, sin = ctx.saved_tensors
             dqkv = flash_attn_bwd(do.contiguous(), qk, qkv, o, lse, seq_len, hq, hkv, d)
             kernels().rope_bwd_(dqkv, cos, sin, seq_len, hq, hkv, d)
-            return dqkv, None, None, None, None, None, None
+            return dqkv, None, None, None, None, None, None, None, None
         qkv, cos, sin = ctx.saved_tensors
         with torch.enable_grad():
             x = qkv.detach().requires_grad_(True)
             o = attention_reference(x, cos, sin, seq_len, hq, hkv, d)
             (dx,) = torch.autograd.grad(o, (x,), do)
-        return dx, None, None, None, None, None, None
+        return dx, None, None, None, None, None, None, None, None
 
 
-def rope_attention(qkv, cos, sin, seq_len, hq, hkv, d):
-    return RopeAttentionFn.apply(qkv, cos, sin, seq_len, hq, hkv, d)
+def rope_attention(qkv, cos, sin, seq_len, hq, hkv, d, keep: Optional[AttentionKeep] = None, gen: int = -1):
+    """RoPE on the packed projection, then causal GQA attention. ``keep``/``gen``: selective
+    activation checkpointing (see :class:`AttentionKeep`)."""
+    return RopeAttentionFn.apply(qkv, cos, sin, seq_len, hq, hkv, d, keep, gen)
 
 
 # --------------------------------------------------------------------------------------

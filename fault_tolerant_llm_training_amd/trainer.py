@@ -254,7 +254,8 @@ def train(args) -> int:
     margs = model_args_for(args.model, vocab_size=holder["vocab"], seq_len=args.sequence_length)
     model = build_model(margs, device, model_dtype, seed=args.seed)
     if args.activation_checkpointing:
-        model.set_activation_checkpointing(args.activation_checkpointing)
+        model.set_activation_checkpointing(args.activation_checkpointing,
+                                           recompute_attention=getattr(args, "recompute_attention", False))
         logger.info(f"Activation checkpointing: recomputing {model.recompute_layers} of {model.n_layers} blocks")
     if checkpoint is not None:
         restore_model(model, checkpoint["model"])

@@ -209,6 +209,12 @@ def build_parser() -> argparse.ArgumentParser:
         "storing their activations (long sequences / larger batches per GPU)",
     )
     parser.add_argument(
+        "--recompute-attention",
+        action="store_true",
+        help="With --activation-checkpointing: also re-run the flash-attention forward in backward "
+        "(default keeps each recomputed block's attention output: one T x Hq x D tensor per block)",
+    )
+    parser.add_argument(
         "--profile-steps",
         type=str,
         default="",

@@ -207,9 +207,9 @@ def test_activation_checkpointing_bitwise():
     tok = torch.randint(0, 512, (2, 128), device="cuda")
     lab = torch.randint(0, 512, (2, 128), device="cuda")
     out = []
-    for n in (0, -1):
+    for n, recompute_attention in ((0, False), (-1, False), (-1, True)):
         m = build_model(a, "cuda", torch.bfloat16, seed=11)
-        m.set_activation_checkpointing(n)
+        m.set_activation_checkpointing(n, recompute_attention=recompute_attention)
         red = GradReducer(m.flat, m.sinks_in_backward_order(), bucket_mb=0.25)
         opt = FlatAdamW(m.parameters(), m.flat, lr=1e-2, max_grad_norm=1.0, reducer=red)
         m.gate = opt.gate
@@ -223,8 +223,9 @@ def test_activation_checkpointing_bitwise():
         opt.gate.wait_all()
         torch.cuda.synchronize()
         out.append((m.flat.params.clone(), opt.exp_avg.clone(), torch.stack(losses)))
-    for x, y in zip(*out):
-        assert torch.equal(x, y)
+    for other in out[1:]:
+        for x, y in zip(out[0], other):
+            assert torch.equal(x, y)
 
 
 @pytest.mark.parametrize("dw_mode", ["all", "none"])

@@ -108,19 +108,46 @@ def test_layernorm_variant():
     assert m.flat.grads.abs().sum() > 0
 
 
+@pytest.mark.parametrize("recompute_attention", [False, True])
 @pytest.mark.parametrize("n", [1, -1])
-def test_activation_checkpointing_same_loss_and_grads(n):
-    """Recomputing blocks in backward (--activation-checkpointing) changes nothing."""
+def test_activation_checkpointing_same_loss_and_grads(n, recompute_attention):
+    """Recomputing blocks in backward (--activation-checkpointing), with or without keeping the
+    attention output, changes nothing."""
     a = model_args_for("tiny", vocab_size=128, seq_len=32)
     tok = torch.randint(0, 128, (2, 32))
     lab = torch.randint(0, 128, (2, 32))
     out = []
     for k in (0, n):
         m = build_model(a, "cpu", torch.float32, seed=5)
-        m.set_activation_checkpointing(k)
+        m.set_activation_checkpointing(k, recompute_attention=recompute_attention)
         loss = m(tok, lab)
         loss.backward()
         out.append((loss.detach(), m.flat.grads.clone()))
     assert m.recompute_layers == (a.n_layers if n < 0 else n)
     assert torch.equal(out[0][0], out[1][0])
     assert torch.allclose(out[0][1], out[1][1], rtol=0, atol=1e-6)
+
+
+def test_selective_checkpointing_skips_attention_recompute(monkeypatch):
+    """Kept attention outputs: the backward recompute runs no attention forward, a forward whose
+    backward never ran leaves nothing stale, and gradients match the no-recompute model."""
+    from fault_tolerant_llm_training_amd.ops import functional as Fx
+
+    calls = []
+    real = Fx.attention_reference
+    monkeypatch.setattr(Fx, "attention_reference", lambda *x: calls.append(1) or real(*x))
+    a = model_args_for("tiny", vocab_size=128, seq_len=32)
+    tok = torch.randint(0, 128, (2, 32))
+    lab = torch.randint(0, 128, (2, 32))
+    ref = build_model(a, "cpu", torch.float32, seed=5)
+    ref(tok, lab).backward()
+    for recompute_attention, per_step in ((False, a.n_layers), (True, 2 * a.n_layers)):
+        m = build_model(a, "cpu", torch.float32, seed=5)
+        m.set_activation_checkpointing(-1, recompute_attention=recompute_attention)
+        m(tok[:, :16], lab[:, :16])  # forward only (no backward): its kept outputs go stale
+        calls.clear()
+        m(tok, lab).backward()
+        # the CPU backward of attention re-derives it under autograd: one call per block
+        assert len(calls) == per_step + a.n_layers
+        assert torch.allclose(m.flat.grads, ref.flat.grads, rtol=0, atol=1e-6)
+        assert all(l.attn_keep.o is None for l in m.layers.values()) or recompute_attention
