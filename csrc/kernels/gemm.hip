@@ -419,6 +419,149 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel(GemmArgs p) {
   }
 }
 
+// ---- 128 x 128 tiles: the small-model GEMMs ---------------------------------------------------
+// Products with fewer than 128 output tiles of 256 x 256 (GPT-2-class d = 768 / 1024 at
+// T = 2048: 24-96 tiles) or M / N not multiples of 256. A 256-thread workgroup (4 waves,
+// 2 x 2, each 64 x 64 = 4 x 4 fragments, 64 fp32 acc VGPRs) owns a 128 x 128 tile, 4x the
+// workgroups of the 256 kernel; two LDS stages of 32 KiB (A + B, BK = 64) filled by LDS-DMA,
+// two workgroups per CU. One barrier per K-tile (see the loop). Tall K with few tiles splits
+// K (pick_splits128). Same operand layouts, swizzles, fragment map and epilogues as the 256
+// kernel; M/N-contiguous operand images are [64][128] (256-B k-rows: the swz_mn XOR stays in
+// a row). Measured (profiles/r2_gemm_small_tiles.log): 1.4-2x the 256 kernel on those shapes
+// but 0.6-1.0x hipBLASLt, so the default routing keeps hipBLASLt for them (ops/functional.py).
+constexpr int S_T = 128, S_NT = 256;
+constexpr int S_OP = S_T * BK * 2;  // 16 KiB
+constexpr int S_STAGE = 2 * S_OP;
+
+template <bool KC>
+__device__ __forceinline__ void stage_tile128(const bf16_t* __restrict__ src, long ld, char* lds, int wid,
+                                              int lane) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int blk = i * 4 + wid;  // 1 KiB block of the 16 KiB image
+    const bf16_t* g;
+    if constexpr (KC) {
+      const int r = blk * 8 + (lane >> 3);
+      const int c = (lane & 7) ^ (r & 7);
+      g = src + (long)r * ld + c * 8;
+    } else {
+      const int k = blk * 4 + (lane >> 4);
+      const int u = (lane & 15) ^ swz_mn(k);
+      g = src + (long)k * ld + u * 8;
+    }
+    glds16(g, lds + blk * 1024);
+  }
+}
+
+template <bool KC>
+__device__ __forceinline__ bf16x8_t frag128(const char* img, int r0, int kk, int lane) {
+  if constexpr (KC) {
+    return frag<true>(img, r0, kk, lane);
+  } else {
+    const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+    const int k = kk * 32 + 8 * g + q;
+    const int u = (r0 >> 3) + (p >> 1);
+    const int half = (p & 1) * 8;
+    const bf16x4_t lo = ds_tr(img + k * 256 + ((u ^ swz_mn(k)) << 4) + half);
+    const bf16x4_t hi = ds_tr(img + (k + 4) * 256 + ((u ^ swz_mn(k + 4)) << 4) + half);
+    bf16x8_t r;
+    r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+    r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+    return r;
+  }
+}
+
+template <bool AK, bool BKC, int EPI, bool RES>
+__global__ __launch_bounds__(S_NT, 2) void gemm128_kernel(GemmArgs p) {
+  constexpr int NS = 2;  // 3-4 stages (1 workgroup per CU) measured slower: profiles/r2_gemm_small_tiles.log
+  __shared__ __attribute__((aligned(1024))) char smem[NS * S_STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 1, wc = wid & 1;
+  int tm, tn;
+  tile_of(blockIdx.x, p.tiles_m, p.tiles_n, tm, tn);
+  const int m0 = tm * S_T, n0 = tn * S_T;
+  const int kz = blockIdx.y * p.k_per_split;
+  const int nk = p.k_per_split / BK;
+
+  const bf16_t* a_src = AK ? p.a + (long)m0 * p.lda + kz : p.a + (long)kz * p.lda + m0;
+  const long a_step = AK ? (long)BK : (long)BK * p.lda;
+  const bf16_t* b_src = BKC ? p.b + (long)n0 * p.ldb + kz : p.b + (long)kz * p.ldb + n0;
+  const long b_step = BKC ? (long)BK : (long)BK * p.ldb;
+  auto stage = [&](int t) {
+    char* base = smem + (t % NS) * S_STAGE;
+    stage_tile128<AK>(a_src + t * a_step, p.lda, base, wid, lane);
+    stage_tile128<BKC>(b_src + t * b_step, p.ldb, base + S_OP, wid, lane);
+  };
+
+  f32x4_t acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  // X / Y: fragments of k-steps 0 / 1 of a K-tile. Y's LDS reads are in flight while X's 16
+  // MFMAs run, the next tile's X reads while Y's run; the barrier between (after X) publishes
+  // tile t + 1 and retires every wave's reads of tile t, whose buffer then takes tile t + NS.
+  bf16x8_t xa[4], xb[4], ya[4], yb[4];
+  auto rd = [&](const char* st, int kk, bf16x8_t(&fa)[4], bf16x8_t(&fb)[4]) {
+    static_for<4>([&](auto I) { fa[I] = frag128<AK>(st, wr * 64 + I * 16, kk, lane); });
+    static_for<4>([&](auto J) { fb[J] = frag128<BKC>(st + S_OP, wc * 64 + J * 16, kk, lane); });
+  };
+  auto mma = [&](bf16x8_t(&fa)[4], bf16x8_t(&fb)[4]) {
+    static_for<4>([&](auto I) {
+      static_for<4>([&](auto J) {
+        acc[I][J] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[J], fa[I], acc[I][J], 0, 0, 0);
+      });
+    });
+  };
+#pragma unroll
+  for (int t = 0; t < NS; ++t)
+    if (t < nk) stage(t);
+  if (nk > 1)
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  rd(smem, 0, xa, xb);
+  for (int t = 0; t < nk; ++t) {
+    const char* cur = smem + (t % NS) * S_STAGE;
+    rd(cur, 1, ya, yb);
+    mma(xa, xb);
+    if (t + 1 < nk) {
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");  // tile t + 1 landed
+      if (t + NS < nk) stage(t + NS);
+      rd(smem + ((t + 1) % NS) * S_STAGE, 0, xa, xb);
+    }
+    mma(ya, yb);
+  }
+
+  const int lr = lane & 15, lc = (lane >> 4) * 4;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = m0 + wr * 64 + i * 16 + lr;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = n0 + wc * 64 + j * 16 + lc;
+      f32x4_t v = acc[i][j];
+      if constexpr (EPI == EPI_F32) {
+        *reinterpret_cast<f32x4_t*>(p.ws + (long)blockIdx.y * p.M * p.N + (long)m * p.N + n) = v;
+      } else {
+        if constexpr (RES) {
+          const uint2 rv = *reinterpret_cast<const uint2*>(p.r + (long)m * p.ldr + n);
+          v[0] += __uint_as_float(rv.x << 16);
+          v[1] += __uint_as_float(rv.x & 0xffff0000u);
+          v[2] += __uint_as_float(rv.y << 16);
+          v[3] += __uint_as_float(rv.y & 0xffff0000u);
+        }
+        uint2 o;
+        o.x = pack2(v[0], v[1]);
+        o.y = pack2(v[2], v[3]);
+        *reinterpret_cast<uint2*>(p.c + (long)m * p.ldc + n) = o;
+      }
+    }
+  }
+}
+
 // Split-K reduction: out = sum_z ws[z] (+ residual), bf16; 8 outputs per thread.
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ ws, int splits,
                                                             long MN, int N, bf16_t* __restrict__ c, long ldc,
@@ -456,6 +599,16 @@ void launch(const GemmArgs& a, int splits, hipStream_t s) {
     hipLaunchKernelGGL((gemm_kernel<AK, BKC, EPI, false>), dim3(a.tiles_m * a.tiles_n, splits), dim3(NT), 0, s, a);
 }
 
+int g_tile = 0;     // 0: pick per shape; 128 / 256: force (scripts/gemm_bench.py A/B)
+template <bool AK, bool BKC, int EPI>
+void launch128(const GemmArgs& a, int splits, hipStream_t s) {
+  const dim3 g(a.tiles_m * a.tiles_n, splits), b(S_NT);
+  if (EPI == EPI_STORE && a.r != nullptr)
+    hipLaunchKernelGGL((gemm128_kernel<AK, BKC, EPI, true>), g, b, 0, s, a);
+  else
+    hipLaunchKernelGGL((gemm128_kernel<AK, BKC, EPI, false>), g, b, 0, s, a);
+}
+
 // Splits so that tiles x splits reaches about the CU count (256) without slicing K below 1024;
 // a tall-K product with few output tiles (GPT-2's LM-head dX: 24 tiles, K = 131072) goes to
 // ~2 workgroups per CU, where the fp32 slabs are still small next to the GEMM.
@@ -463,6 +616,13 @@ int pick_splits(int tiles, int K) {
   int s = 1;
   const int target = tiles < 64 ? 400 : 200;
   while (tiles * s < target && (K / (s * 2)) % BK == 0 && K / (s * 2) >= 1024) s *= 2;
+  return s;
+}
+
+// 128 tiles: split K (>= 512 per split) while the grid is under the CU count.
+int pick_splits128(int tiles, int K) {
+  int s = 1;
+  while (tiles * s < 256 && (K / (s * 2)) % BK == 0 && K / (s * 2) >= 512) s *= 2;
   return s;
 }
 
@@ -479,8 +639,13 @@ at::Tensor gemm(const at::Tensor& a, bool a_kc, const at::Tensor& b, bool b_kc, 
   FT_CHECK_BF16(b);
   FT_CHECK_CONTIG(a);
   FT_CHECK_CONTIG(b);
-  TORCH_CHECK(M % BM == 0 && N % BN == 0 && K % BK == 0, "gemm: M, N must be multiples of 256 and K of 64 (got ",
+  TORCH_CHECK(M % S_T == 0 && N % S_T == 0 && K % BK == 0, "gemm: M, N must be multiples of 128 and K of 64 (got ",
               M, " ", N, " ", K, ")");
+  // 256 x 256 tiles when they fill the chip (>= 128 tiles) or split-K over a tall K does;
+  // 128 x 128 tiles otherwise (4x the workgroups)
+  const bool fits256 = M % BM == 0 && N % BN == 0;
+  const bool big = g_tile == 256 || (g_tile == 0 && fits256 && ((M / BM) * (N / BN) >= 128 || K >= 16384));
+  TORCH_CHECK(!big || fits256, "gemm: 256 tiles need M, N multiples of 256");
   TORCH_CHECK(a.numel() == M * K && b.numel() == N * K, "gemm: operand sizes do not match M, N, K");
   const at::DeviceGuard guard(a.device());
   at::Tensor c;
@@ -514,9 +679,10 @@ at::Tensor gemm(const at::Tensor& a, bool a_kc, const at::Tensor& b, bool b_kc, 
   p.M = M;
   p.N = N;
   p.K = K;
-  p.tiles_m = M / BM;
-  p.tiles_n = N / BN;
-  int s = splits > 0 ? (int)splits : pick_splits(p.tiles_m * p.tiles_n, K);
+  const int tile = big ? BM : S_T;
+  p.tiles_m = M / tile;
+  p.tiles_n = N / tile;
+  int s = splits > 0 ? (int)splits : (big ? pick_splits(p.tiles_m * p.tiles_n, K) : pick_splits128(p.tiles_m * p.tiles_n, K));
   TORCH_CHECK(K % (s * BK) == 0, "gemm: K must split into multiples of 64");
   p.k_per_split = K / s;
   hipStream_t st = ft_stream();
@@ -526,7 +692,11 @@ at::Tensor gemm(const at::Tensor& a, bool a_kc, const at::Tensor& b, bool b_kc, 
     p.ws = mptr<float>(ws);
   }
 #define FT_GEMM_LAUNCH(AK_, BK_)                                                             \
-  if (s > 1)                                                                                 \
+  if (!big && s > 1)                                                                         \
+    launch128<AK_, BK_, EPI_F32>(p, s, st);                                                  \
+  else if (!big)                                                                             \
+    launch128<AK_, BK_, EPI_STORE>(p, s, st);                                                \
+  else if (s > 1)                                                                            \
     launch<AK_, BK_, EPI_F32>(p, s, st);                                                     \
   else                                                                                       \
     launch<AK_, BK_, EPI_STORE>(p, s, st);
@@ -653,7 +823,14 @@ at::Tensor gemm_ablate(const at::Tensor& a, const at::Tensor& b, int64_t M, int6
   return c;
 }
 
+// A/B hook: tile 0 (per shape) / 128 / 256.
+void gemm_config(int64_t tile) {
+  TORCH_CHECK(tile == 0 || tile == 128 || tile == 256, "gemm_config: tile 0, 128 or 256");
+  g_tile = (int)tile;
+}
+
 TORCH_LIBRARY_FRAGMENT(ftamd, m) {
+  m.def("gemm_config(int tile) -> ()", &gemm_config);
   m.def("gemm_ablate(Tensor a, Tensor b, int M, int N, int K, int abl) -> Tensor", &gemm_ablate);
   m.def(
       "gemm(Tensor a, bool a_kc, Tensor b, bool b_kc, int M, int N, int K, Tensor(a!)? out, Tensor? residual, "

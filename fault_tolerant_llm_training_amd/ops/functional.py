@@ -53,7 +53,7 @@ def _hand(kind: str, M: int, N: int, K: int, *ts) -> bool:
     """Use the hand GEMM for product ``kind`` ("fwd", "dx", "dw", "ffn") of shape M x N x K?"""
     if _GEMM_MODE == "blas" or not all(t.is_cuda and t.dtype == torch.bfloat16 for t in ts):
         return False
-    if M % 256 or N % 256 or K % 64:
+    if M % 128 or N % 128 or K % 64:  # 256 x 256 tiles where they fill the chip, else 128 x 128
         return False
     if _GEMM_MODE == "hand" or kind in _HAND_AUTO:
         return True

@@ -29,10 +29,21 @@ def check(out, ref, K_):
     assert rel < 8e-3, rel
 
 
+@pytest.fixture(params=[256, 128], ids=["tile256", "tile128"])
+def tile(request):
+    """Force the 256 x 256 or the 128 x 128 kernel (the default picks per shape)."""
+    K().gemm_config(request.param)
+    yield request.param
+    K().gemm_config(0)
+
+
 @pytest.mark.parametrize("a_kc,b_kc", [(True, True), (True, False), (False, False), (False, True)])
 @pytest.mark.parametrize("M,N,Kd,splits", [(256, 256, 64, 1), (512, 768, 320, 1), (768, 512, 1024, 2),
-                                           (512, 1024, 2048, 0), (1024, 256, 4096, 4)])
-def test_gemm_layouts(a_kc, b_kc, M, N, Kd, splits):
+                                           (512, 1024, 2048, 0), (1024, 256, 4096, 4), (384, 640, 192, 1),
+                                           (128, 384, 2048, 0)])
+def test_gemm_layouts(tile, a_kc, b_kc, M, N, Kd, splits):
+    if M % tile or N % tile:
+        pytest.skip("shape not a multiple of the tile")
     torch.manual_seed(M + N + Kd)
     A = rnd(M, Kd)
     B = rnd(Kd, N) + torch.arange(N, device="cuda").bfloat16() * 1e-3  # asymmetric
@@ -43,7 +54,7 @@ def test_gemm_layouts(a_kc, b_kc, M, N, Kd, splits):
 
 
 @pytest.mark.parametrize("splits", [1, 2])
-def test_gemm_residual_and_accumulate(splits):
+def test_gemm_residual_and_accumulate(tile, splits):
     M, N, Kd = 512, 512, 1024
     A, B, R = rnd(M, Kd), rnd(N, Kd), rnd(M, N)
     ref = A.float() @ B.float().t()
@@ -52,6 +63,19 @@ def test_gemm_residual_and_accumulate(splits):
     C = R.clone()
     K().gemm(A, True, B, True, M, N, Kd, C, None, True, splits)
     check(C, ref + R.float(), Kd)
+
+
+def test_gemm_tile_choice_gpt2_shapes():
+    """Default tile choice on GPT-2-small shapes (128 tiles where 256 tiles underfill), all
+    layouts, against fp32."""
+    for M, N, Kd in ((2048, 768, 768), (2048, 2304, 768), (768, 768, 2048)):
+        A = rnd(M, Kd)
+        B = rnd(Kd, N)
+        for a_kc, b_kc in ((True, True), (True, False), (False, False)):
+            a_arg = A.contiguous() if a_kc else A.t().contiguous()
+            b_arg = B.t().contiguous() if b_kc else B.contiguous()
+            out = K().gemm(a_arg, a_kc, b_arg, b_kc, M, N, Kd, None, None, False, 0)
+            check(out, A.float() @ B.float(), Kd)
 
 
 def test_gemm_swiglu_forward_and_backward():
