@@ -171,9 +171,6 @@ class GradReducer:
                 b.shard_len = b.numel // self.world
                 b.shard_lo = self.shard_numel
                 self.shard_numel += b.shard_len
-            self.grad_shard = torch.zeros(self.shard_numel, dtype=flat.dtype, device=flat.device)
-        else:
-            self.grad_shard = None
         self.side = torch.cuda.Stream(device=flat.device) if self.overlap else None
         if self.cuda:
             for b in self.buckets:
@@ -197,12 +194,17 @@ class GradReducer:
         lo = b.lo + self.rank * b.shard_len
         return self.flat.params[lo : lo + b.shard_len]
 
+    def grad_shard(self, b: Bucket) -> torch.Tensor:
+        """This rank's 1/W of bucket b's gradient: the in-place reduce-scatter's output (RCCL
+        runs it in place when the output is the rank's own chunk of the input — no separate
+        shard buffer, no local copy of that chunk)."""
+        lo = b.lo + self.rank * b.shard_len
+        return self.flat.grads[lo : lo + b.shard_len]
+
     def grad_for_update(self, b: Bucket) -> torch.Tensor:
         if self.mode == "zero1":
-            if b.sparse:  # full (already summed) gradient is replicated: take this rank's slice
-                lo = b.lo + self.rank * b.shard_len
-                return self.flat.grads[lo : lo + b.shard_len]
-            return self.grad_shard[b.shard_lo : b.shard_lo + b.shard_len]
+            # sparse bucket: the full (already summed) gradient is replicated; the rank's slice
+            return self.grad_shard(b)
         return self.flat.grads[b.lo : b.hi]
 
     def _gather_rows(self, tokens: torch.Tensor, dy: torch.Tensor):
@@ -293,9 +295,8 @@ class GradReducer:
         elif self.mode == "allreduce":
             b.work = dist.all_reduce(grads, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
         elif self.mode == "zero1":
-            out = self.grad_shard[b.shard_lo : b.shard_lo + b.shard_len]
-            b.work = dist.reduce_scatter_tensor(out, grads, op=dist.ReduceOp.SUM, group=self.group,
-                                                async_op=True)
+            b.work = dist.reduce_scatter_tensor(self.grad_shard(b), grads, op=dist.ReduceOp.SUM,
+                                                group=self.group, async_op=True)
         if not self.overlap:
             return  # CPU / no side stream: sums are taken in finish()
         side = self.side
