@@ -89,7 +89,9 @@ def main():
     from fault_tolerant_llm_training_amd.utils.lr import build_lr_scheduler
     from fault_tolerant_llm_training_amd.data.synthetic import SyntheticTokens
 
-    info = fdist.init_distributed(a.device)
+    # 5-minute collective timeout: a rank that fails inside the checkpoint block makes its peers
+    # raise (and report the error in the JSON line) instead of blocking for the 30-minute default
+    info = fdist.init_distributed(a.device, timeout_s=300)
     dev = info.device
     if os.environ.get("FT_COMPUTE_PRIORITY") == "1" and dev.type == "cuda":
         # compute on a high-priority stream: its workgroups are dispatched ahead of the
