@@ -34,6 +34,12 @@ def t(fn, it=20):
 
 tf = t(lambda: K.flash_fwd(qk, qkv, S, Hq, Hkv, D))
 print(f"fwd {tf:7.1f} us  {2 * unit / tf / 1e6:6.0f} TF/s")
+if hasattr(K, "flash_set_fwd_split"):  # forward key split forced off / on (default: auto)
+    for v in (0, 1):
+        K.flash_set_fwd_split(v)
+        tf = t(lambda: K.flash_fwd(qk, qkv, S, Hq, Hkv, D))
+        print(f"fwd key split {'on ' if v else 'off'} {tf:7.1f} us  {2 * unit / tf / 1e6:6.0f} TF/s")
+    K.flash_set_fwd_split(-1)
 for mode, name in ((0, "bwd atomics"), (1, "bwd deterministic"), (2, "bwd no-atomic (racy, timing only)")):
     tb = t(lambda: K.flash_bwd(do, qk, qkv, o, lse, S, Hq, Hkv, D, mode))
     print(f"{name:34s} {tb:7.1f} us  {5 * unit / tb / 1e6:6.0f} TF/s (5-matmul count)")
@@ -42,3 +48,9 @@ if hasattr(K, "flash_set_dkdv2"):
     tb = t(lambda: K.flash_bwd(do, qk, qkv, o, lse, S, Hq, Hkv, D, 1))
     print(f"{'bwd deterministic, 1-slice dK/dV':34s} {tb:7.1f} us  {5 * unit / tb / 1e6:6.0f} TF/s (5-matmul count)")
     K.flash_set_dkdv2(True)
+if hasattr(K, "flash_set_dq_split"):  # dQ key split forced off / on (default: auto)
+    for v in (0, 1):
+        K.flash_set_dq_split(v)
+        tb = t(lambda: K.flash_bwd(do, qk, qkv, o, lse, S, Hq, Hkv, D, 1))
+        print(f"bwd deterministic, dQ split {'on ' if v else 'off'} {tb:7.1f} us  {5 * unit / tb / 1e6:6.0f} TF/s")
+    K.flash_set_dq_split(-1)

@@ -102,3 +102,62 @@ def test_flash_fwd_growing_scores(slope):
                    v.bfloat16().float().view(1, S, Hkv, D))
     assert torch.isfinite(o).all()
     assert rel(o.view(1, S, Hq, D), ref) < 1e-2
+
+
+@pytest.mark.parametrize("B,S,Hq,Hkv,D", [(1, 2048, 12, 12, 64), (2, 320, 8, 2, 128), (1, 100, 4, 4, 64),
+                                         (1, 33, 2, 1, 128), (1, 4096, 4, 1, 128)])
+def test_flash_fwd_key_split_matches(B, S, Hq, Hkv, D):
+    """The key-split forward (two half-blocks over even / odd key tiles, merged in LDS) equals the
+    one-pass forward up to summation order, incl. query tiles whose odd half sees no key, and its
+    log-sum-exp drives the backward the same way."""
+    from fault_tolerant_llm_training_amd._native import kernels
+
+    K = kernels()
+    torch.manual_seed(3)
+    T = B * S
+    qkv = torch.randn(T, (Hq + 2 * Hkv) * D, device="cuda").bfloat16()
+    qk = torch.randn(T, (Hq + Hkv) * D, device="cuda").bfloat16()
+    try:
+        K.flash_set_fwd_split(0)
+        o0, l0 = K.flash_fwd(qk, qkv, S, Hq, Hkv, D)
+        K.flash_set_fwd_split(1)
+        o1, l1 = K.flash_fwd(qk, qkv, S, Hq, Hkv, D)
+    finally:
+        K.flash_set_fwd_split(-1)
+    assert torch.isfinite(o1).all()
+    assert rel(o1, o0) < 4e-3
+    Sp = l0.shape[-1]
+    valid = torch.arange(Sp, device="cuda") < S
+    assert (l1[..., valid] - l0[..., valid]).abs().max().item() < 1e-3
+    do = torch.randn(T, Hq * D, device="cuda").bfloat16()
+    g0 = K.flash_bwd(do, qk, qkv, o0, l0, S, Hq, Hkv, D, 1)
+    g1 = K.flash_bwd(do, qk, qkv, o1, l1, S, Hq, Hkv, D, 1)
+    assert rel(g1, g0) < 1e-2
+
+
+@pytest.mark.parametrize("B,S,Hq,Hkv,D", [(1, 2048, 12, 12, 64), (2, 320, 8, 2, 128), (1, 100, 4, 4, 64),
+                                         (1, 4096, 4, 1, 128)])
+def test_flash_dq_key_split_matches(B, S, Hq, Hkv, D):
+    """The key-split dQ kernel (two half-blocks, partials added in LDS in a fixed order) equals
+    the one-pass dQ up to summation order and is bit-reproducible; dK / dV are untouched."""
+    from fault_tolerant_llm_training_amd._native import kernels
+
+    K = kernels()
+    torch.manual_seed(4)
+    T = B * S
+    qkv = torch.randn(T, (Hq + 2 * Hkv) * D, device="cuda").bfloat16()
+    qk = torch.randn(T, (Hq + Hkv) * D, device="cuda").bfloat16()
+    do = torch.randn(T, Hq * D, device="cuda").bfloat16()
+    o, lse = K.flash_fwd(qk, qkv, S, Hq, Hkv, D)
+    try:
+        K.flash_set_dq_split(0)
+        g0 = K.flash_bwd(do, qk, qkv, o, lse, S, Hq, Hkv, D, 1)
+        K.flash_set_dq_split(1)
+        g1 = K.flash_bwd(do, qk, qkv, o, lse, S, Hq, Hkv, D, 1)
+        g2 = K.flash_bwd(do, qk, qkv, o, lse, S, Hq, Hkv, D, 1)
+    finally:
+        K.flash_set_dq_split(-1)
+    assert torch.equal(g1, g2)
+    nq = Hq * D
+    assert rel(g1[:, :nq], g0[:, :nq]) < 4e-3
+    assert torch.equal(g1[:, nq:], g0[:, nq:])
