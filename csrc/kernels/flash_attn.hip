@@ -661,16 +661,19 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_kernel(
 // wave per SIMD there is no other wave to fill the MFMA pipe during a softmax phase).
 // Q | dO pairs by LDS-DMA, double-buffered in two LDS objects (loop unrolled by two);
 // the slices' lse / delta ride along in LDS (registers are the scarce resource here).
-template <int D, int NW = 4>
-__global__ __launch_bounds__(64 * NW, 4 / NW) void flash_bwd_dkdv2_kernel(
+// SPLIT = 2: two half-blocks take alternate slice pairs of the same keys and add their dK / dV
+// partials through LDS at the end (fixed order: bit-reproducible), halving the longest
+// (first) key block's sweep.
+template <int D, int NW = 4, int SPLIT = 1>
+__global__ __launch_bounds__(64 * NW * SPLIT, SPLIT == 1 ? 4 / NW : 8 / (NW * SPLIT)) void flash_bwd_dkdv2_kernel(
     const bf16_t* __restrict__ dO, const bf16_t* __restrict__ qk, const bf16_t* __restrict__ qkv,
     const float* __restrict__ lse2, const float* __restrict__ delta, bf16_t* __restrict__ dk_part,
     bf16_t* __restrict__ dv_part, int B, int S, int Hq, int Hkv, float sl2, float scale) {
   constexpr int BK = 32 * NW, BQ = 32, KS = D / 16, NDB = D / 32;
   constexpr int QIMG = BQ * D * 2;          // one Q or dO slice
   constexpr int SLOT = 2 * QIMG + 256;      // Q | dO | lse[32] | delta[32] of one slice
-  __shared__ __attribute__((aligned(16))) char pb0[2 * SLOT];  // pair buffer 0: slice A | slice B
-  __shared__ __attribute__((aligned(16))) char pb1[2 * SLOT];  // pair buffer 1
+  __shared__ __attribute__((aligned(16))) char pb0[2 * SLOT * SPLIT];  // pair buffer 0: slice A | slice B
+  __shared__ __attribute__((aligned(16))) char pb1[2 * SLOT * SPLIT];  // pair buffer 1 (per half-block)
 
   const int per = B * Hq;
   const int L = blockIdx.x;
@@ -680,7 +683,8 @@ __global__ __launch_bounds__(64 * NW, 4 / NW) void flash_bwd_dkdv2_kernel(
   int h, kvh;
   map_head(rem % Hq, Hq, Hkv, h, kvh);
 
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, l32 = lane & 31, hi = lane >> 5;
+  const int tid = threadIdx.x, lane = tid & 63, l32 = lane & 31, hi = lane >> 5;
+  const int hs = (tid >> 6) / NW, wave = (tid >> 6) % NW;  // half-block (pair parity), key group
   const int kb0 = kt * BK;
   const int kw = kb0 + wave * 32;  // this wave's first key
   const long ldqk = (long)(Hq + Hkv) * D, ldv = (long)(Hq + 2 * Hkv) * D, ldo = (long)Hq * D;
@@ -799,17 +803,24 @@ __global__ __launch_bounds__(64 * NW, 4 / NW) void flash_bwd_dkdv2_kernel(
       fin(sl, i, sv, dpv, std::false_type{});
   };
 
-  dma(0, pb0);
+  char* const b0 = pb0 + hs * 2 * SLOT;
+  char* const b1 = pb1 + hs * 2 * SLOT;
+  if (hs < npairs) dma(hs, b0);
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
-  auto iter = [&](const int p, auto BUF) __attribute__((always_inline)) {
+  // iteration it: this half-block's pair it * SPLIT + hs (both halves run the same number of
+  // iterations so their barriers pair up; one may idle in the last)
+  auto iter = [&](const int it, auto BUF) __attribute__((always_inline)) {
     constexpr int bb = decltype(BUF)::value;
-    char* cur = bb ? pb1 : pb0;
-    if (p + 1 < npairs) dma(p + 1, bb ? pb0 : pb1);
+    const int p = it * SPLIT + hs;
+    char* cur = bb ? b1 : b0;
+    if (p + SPLIT < npairs) dma(p + SPLIT, bb ? b0 : b1);
     const int ia = 2 * p, ib = 2 * p + 1;
     const int qa = (qs0 + ia) * BQ;
     // steady state: both slices entirely below this wave's diagonal and inside S
-    if (ib < n && qa >= kw + 31 && qa + 2 * BQ <= S) {
+    if (p >= npairs) {
+      // idle (this half-block has no pair left)
+    } else if (ib < n && qa >= kw + 31 && qa + 2 * BQ <= S) {
       f32x16_t sa, dpa, sb, dpb;
       // the compiler's default schedule keeps the pair's phases apart; the IGLP
       // "DS + MFMA interleave" strategy spreads the LDS reads and the VALU between the
@@ -827,9 +838,33 @@ __global__ __launch_bounds__(64 * NW, 4 / NW) void flash_bwd_dkdv2_kernel(
     __builtin_amdgcn_s_waitcnt(0);  // this wave's DMA of pair p+1 has landed ...
     __syncthreads();                // ... and everyone's; nobody reads pair p any more
   };
-  for (int p = 0; p < npairs; p += 2) {
-    iter(p, std::integral_constant<int, 0>{});
-    if (p + 1 < npairs) iter(p + 1, std::integral_constant<int, 1>{});
+  const int nit = (npairs + SPLIT - 1) / SPLIT;
+  for (int it = 0; it < nit; it += 2) {
+    iter(it, std::integral_constant<int, 0>{});
+    if (it + 1 < nit) iter(it + 1, std::integral_constant<int, 1>{});
+  }
+  if constexpr (SPLIT == 2) {  // half-block 1 parks dK in pb0, dV in pb1; half-block 0 adds
+    float* xk = reinterpret_cast<float*>(pb0) + (wave * 64 + lane);
+    float* xv = reinterpret_cast<float*>(pb1) + (wave * 64 + lane);
+    static_assert(NW * 64 * NDB * 16 * 4 <= 2 * SLOT * SPLIT, "merge buffer");
+    if (hs == 1) {
+#pragma unroll
+      for (int db = 0; db < NDB; ++db)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          xk[(db * 16 + r) * NW * 64] = dk[db][r];
+          xv[(db * 16 + r) * NW * 64] = dv[db][r];
+        }
+    }
+    __syncthreads();
+    if (hs == 1) return;
+#pragma unroll
+    for (int db = 0; db < NDB; ++db)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        dk[db][r] += xk[(db * 16 + r) * NW * 64];
+        dv[db][r] += xv[(db * 16 + r) * NW * 64];
+      }
   }
 
   // dK / dV of this q-head in bf16 (summed over the GQA group by the finalize kernel)
@@ -1077,6 +1112,13 @@ int g_dq_split = [] {
   return e == nullptr ? -1 : std::atoi(e);
 }();
 
+// dK/dV split of the slice-pair kernel: -1 auto, 0 off, 1 on (FT_FLASH_KV_SPLIT /
+// flash_set_kv_split, for A/B).
+int g_kv_split = [] {
+  const char* e = std::getenv("FT_FLASH_KV_SPLIT");
+  return e == nullptr ? -1 : std::atoi(e);
+}();
+
 // Deterministic backward, dK/dV stage: the slice-pair kernel (default) or the one-slice
 // flash_bwd_kernel<D, 1> (FT_FLASH_DKDV2=0 / flash_set_dkdv2, for A/B).
 bool g_dkdv2 = [] {
@@ -1187,11 +1229,14 @@ at::Tensor flash_bwd(const at::Tensor& dout, const at::Tensor& qk, const at::Ten
                      cptr<bf16_t>(qk), cptr<bf16_t>(qkv), cptr<float>(lse), cptr<float>(delta),     \
                      dqp, mptr<bf16_t>(dk_part), mptr<bf16_t>(dv_part), B, (int)S, (int)Hq, (int)Hkv, \
                      sl2, scale)
-#define FT_DKDV2(DD, NW_)                                                                          \
-  hipLaunchKernelGGL((flash_bwd_dkdv2_kernel<DD, NW_>), grid2, block2, 0, ft_stream(), cptr<bf16_t>(dout), \
-                     cptr<bf16_t>(qk), cptr<bf16_t>(qkv), cptr<float>(lse), cptr<float>(delta),         \
-                     mptr<bf16_t>(dk_part), mptr<bf16_t>(dv_part), B, (int)S, (int)Hq, (int)Hkv, sl2,    \
-                     scale)
+  // dK/dV split, head_dim 64 only (at 128 the doubled block spills): FT_FLASH_KV_SPLIT=0/1
+  // forces; default: grids of at most one wave per SIMD
+  const bool kv_split = D == 64 && (g_kv_split >= 0 ? g_kv_split == 1 : (long)grid2.x * nw <= 1024);
+#define FT_DKDV2(DD, NW_, SP_)                                                                             \
+  hipLaunchKernelGGL((flash_bwd_dkdv2_kernel<DD, NW_, SP_>), grid2, dim3(64 * NW_ * SP_), 0, ft_stream(), \
+                     cptr<bf16_t>(dout), cptr<bf16_t>(qk), cptr<bf16_t>(qkv), cptr<float>(lse),           \
+                     cptr<float>(delta), mptr<bf16_t>(dk_part), mptr<bf16_t>(dv_part), B, (int)S,         \
+                     (int)Hq, (int)Hkv, sl2, scale)
   // dQ key split by default (FT_FLASH_DQ_SPLIT=0 turns it off): S = 2048, 12 heads of 64:
   // 94 -> 83 us for the whole backward; 8B layer 173 -> 167 us; S = 16384 1006 -> 972 us
   // (profiles/r2_flash_key_split.log)
@@ -1209,16 +1254,24 @@ at::Tensor flash_bwd(const at::Tensor& dout, const at::Tensor& qk, const at::Ten
     hipLaunchKernelGGL(flash_bwd_pre_kernel<128>, dim3(pre_blocks), block, 0, ft_stream(),
                        cptr<bf16_t>(dout), cptr<bf16_t>(out), mptr<float>(delta), B, (int)S, (int)Hq);
     if (mode == 0) FT_BWD(128, 0);
-    else if (mode == 1) { if (g_dkdv2 && nw == 4) { FT_DKDV2(128, 4); } else FT_BWD(128, 1); FT_DQ(128, 4); }
+    else if (mode == 1) { if (g_dkdv2 && nw == 4) { FT_DKDV2(128, 4, 1); } else FT_BWD(128, 1); FT_DQ(128, 4); }
     else FT_BWD(128, 2);
   } else {
     hipLaunchKernelGGL(flash_bwd_pre_kernel<64>, dim3(pre_blocks), block, 0, ft_stream(),
                        cptr<bf16_t>(dout), cptr<bf16_t>(out), mptr<float>(delta), B, (int)S, (int)Hq);
     if (mode == 0) FT_BWD(64, 0);
-    else if (mode == 1 && nw == 2) { FT_DKDV2(64, 2); FT_DQ(64, 2); }
+    else if (mode == 1 && nw == 2) {
+      if (kv_split) FT_DKDV2(64, 2, 2); else FT_DKDV2(64, 2, 1);
+      FT_DQ(64, 2);
+    }
     // head_dim 64 with 4-wave blocks: the one-slice dK/dV kernel is faster (S = 8192, 16 heads:
     // 631 vs 783 us, profiles/r2_flash_long_context.log); FT_FLASH_DKDV2=2 forces the slice pair
-    else if (mode == 1) { if (g_dkdv2_64) { FT_DKDV2(64, 4); } else FT_BWD(64, 1); FT_DQ(64, 4); }
+    else if (mode == 1) {
+      if (g_dkdv2_64 && kv_split) FT_DKDV2(64, 4, 2);
+      else if (g_dkdv2_64) FT_DKDV2(64, 4, 1);
+      else FT_BWD(64, 1);
+      FT_DQ(64, 4);
+    }
     else FT_BWD(64, 2);
   }
 #undef FT_BWD
@@ -1239,11 +1292,13 @@ void flash_set_dkdv2(bool on) { g_dkdv2 = on; }
 // Same-process A/B switch of the forward key split: -1 auto, 0 off, 1 on.
 void flash_set_fwd_split(int64_t v) { g_fwd_split = (int)v; }
 void flash_set_dq_split(int64_t v) { g_dq_split = (int)v; }
+void flash_set_kv_split(int64_t v) { g_kv_split = (int)v; }
 
 TORCH_LIBRARY_FRAGMENT(ftamd, m) {
   m.def("flash_set_dkdv2(bool on) -> ()", &flash_set_dkdv2);
   m.def("flash_set_fwd_split(int v) -> ()", &flash_set_fwd_split);
   m.def("flash_set_dq_split(int v) -> ()", &flash_set_dq_split);
+  m.def("flash_set_kv_split(int v) -> ()", &flash_set_kv_split);
   m.def("flash_fwd(Tensor qk, Tensor qkv, int S, int Hq, int Hkv, int D) -> (Tensor, Tensor)",
         &flash_fwd);
   m.def(

@@ -54,3 +54,9 @@ if hasattr(K, "flash_set_dq_split"):  # dQ key split forced off / on (default: a
         tb = t(lambda: K.flash_bwd(do, qk, qkv, o, lse, S, Hq, Hkv, D, 1))
         print(f"bwd deterministic, dQ split {'on ' if v else 'off'} {tb:7.1f} us  {5 * unit / tb / 1e6:6.0f} TF/s")
     K.flash_set_dq_split(-1)
+if hasattr(K, "flash_set_kv_split"):  # dK/dV split forced off / on (default: auto, d=64)
+    for v in (0, 1):
+        K.flash_set_kv_split(v)
+        tb = t(lambda: K.flash_bwd(do, qk, qkv, o, lse, S, Hq, Hkv, D, 1))
+        print(f"bwd deterministic, dK/dV split {'on ' if v else 'off'} {tb:7.1f} us  {5 * unit / tb / 1e6:6.0f} TF/s")
+    K.flash_set_kv_split(-1)
