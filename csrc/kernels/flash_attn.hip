@@ -668,7 +668,7 @@ template <int D, int NW = 4, int SPLIT = 1>
 __global__ __launch_bounds__(64 * NW * SPLIT, SPLIT == 1 ? 4 / NW : 8 / (NW * SPLIT)) void flash_bwd_dkdv2_kernel(
     const bf16_t* __restrict__ dO, const bf16_t* __restrict__ qk, const bf16_t* __restrict__ qkv,
     const float* __restrict__ lse2, const float* __restrict__ delta, bf16_t* __restrict__ dk_part,
-    bf16_t* __restrict__ dv_part, int B, int S, int Hq, int Hkv, float sl2, float scale) {
+    bf16_t* __restrict__ dv_part, long ldkv, int B, int S, int Hq, int Hkv, float sl2, float scale) {
   constexpr int BK = 32 * NW, BQ = 32, KS = D / 16, NDB = D / 32;
   constexpr int QIMG = BQ * D * 2;          // one Q or dO slice
   constexpr int SLOT = 2 * QIMG + 256;      // Q | dO | lse[32] | delta[32] of one slice
@@ -867,14 +867,16 @@ __global__ __launch_bounds__(64 * NW * SPLIT, SPLIT == 1 ? 4 / NW : 8 / (NW * SP
       }
   }
 
-  // dK / dV of this q-head in bf16 (summed over the GQA group by the finalize kernel)
+  // dK / dV of this q-head in bf16: per-q-head partials [T, Hq*D] (ldkv = Hq*D) that the
+  // finalize kernel sums over the GQA group, or — without GQA (Hq == Hkv) — straight into the
+  // K / V columns of dqkv (the pointers are offset by the host, ldkv = its row stride)
 #pragma unroll
   for (int db = 0; db < NDB; ++db)
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int k = kw + (r & 3) + 8 * (r >> 2) + 4 * hi;
       if (k < S) {
-        const long off = ((long)b * S + k) * ldo + (long)h * D + db * 32 + l32;
+        const long off = ((long)b * S + k) * ldkv + (long)h * D + db * 32 + l32;
         dk_part[off] = f2bf(dk[db][r] * scale);
         dv_part[off] = f2bf(dv[db][r]);
       }
@@ -1211,23 +1213,32 @@ at::Tensor flash_bwd(const at::Tensor& dout, const at::Tensor& qk, const at::Ten
   // mode 2: timing experiment only (racy dQ stores).
   const bool det = mode == 1;
   at::Tensor dq_acc = det ? at::Tensor() : (mode == 2 ? at::empty({T, Hq * D}, f32) : at::zeros({T, Hq * D}, f32));
-  auto dk_part = at::empty({T, Hq * D}, qk.options());
-  auto dv_part = at::empty({T, Hq * D}, qk.options());
+  const int nw_ = waves_per_block(S, B, Hq, D);
+  // slice-pair dK/dV kernel in the deterministic mode (else the one-slice flash_bwd_kernel)
+  const bool use_dkdv2 = det && (D == 128 ? (g_dkdv2 && nw_ == 4) : (nw_ == 2 || g_dkdv2_64));
+  // no GQA: that kernel writes dK / dV into dqkv itself, dQ comes from the dQ kernel, so the
+  // finalize pass (and the partial buffers) are skipped
+  const bool direct = use_dkdv2 && Hq == Hkv;
   auto dqkv = at::empty({T, (Hq + 2 * Hkv) * D}, qk.options());
+  at::Tensor dk_part = direct ? at::Tensor() : at::empty({T, Hq * D}, qk.options());
+  at::Tensor dv_part = direct ? at::Tensor() : at::empty({T, Hq * D}, qk.options());
+  bf16_t* dkp = direct ? mptr<bf16_t>(dqkv) + (long)Hq * D : mptr<bf16_t>(dk_part);
+  bf16_t* dvp = direct ? mptr<bf16_t>(dqkv) + (long)(Hq + Hkv) * D : mptr<bf16_t>(dv_part);
+  const long ldkv = direct ? (long)(Hq + 2 * Hkv) * D : (long)Hq * D;
   const float sl2 = LOG2E_F / std::sqrt((float)D);
   const float scale = 1.f / std::sqrt((float)D);
   const long rows = (long)T * Hq;
   const int pre_blocks = (int)((rows * 16 + 255) / 256);
   const int nkt = (S + 127) / 128;
   dim3 grid(nkt * B * Hq), block(256);
-  const int nw = waves_per_block(S, B, Hq, D);
+  const int nw = nw_;
   const int nkt2 = (S + 32 * nw - 1) / (32 * nw);  // tiles of the deterministic dK/dV and dQ kernels
   const dim3 grid2(nkt2 * B * Hq), block2(64 * nw);
   float* dqp = det ? nullptr : mptr<float>(dq_acc);
 #define FT_BWD(DD, MODE)                                                                          \
   hipLaunchKernelGGL((flash_bwd_kernel<DD, MODE>), grid, block, 0, ft_stream(), cptr<bf16_t>(dout), \
                      cptr<bf16_t>(qk), cptr<bf16_t>(qkv), cptr<float>(lse), cptr<float>(delta),     \
-                     dqp, mptr<bf16_t>(dk_part), mptr<bf16_t>(dv_part), B, (int)S, (int)Hq, (int)Hkv, \
+                     dqp, dkp, dvp, B, (int)S, (int)Hq, (int)Hkv,                                    \
                      sl2, scale)
   // dK/dV split, head_dim 64 only (at 128 the doubled block spills): FT_FLASH_KV_SPLIT=0/1
   // forces; default: grids of at most one wave per SIMD
@@ -1235,7 +1246,7 @@ at::Tensor flash_bwd(const at::Tensor& dout, const at::Tensor& qk, const at::Ten
 #define FT_DKDV2(DD, NW_, SP_)                                                                             \
   hipLaunchKernelGGL((flash_bwd_dkdv2_kernel<DD, NW_, SP_>), grid2, dim3(64 * NW_ * SP_), 0, ft_stream(), \
                      cptr<bf16_t>(dout), cptr<bf16_t>(qk), cptr<bf16_t>(qkv), cptr<float>(lse),           \
-                     cptr<float>(delta), mptr<bf16_t>(dk_part), mptr<bf16_t>(dv_part), B, (int)S,         \
+                     cptr<float>(delta), dkp, dvp, ldkv, B, (int)S,                                       \
                      (int)Hq, (int)Hkv, sl2, scale)
   // dQ key split by default (FT_FLASH_DQ_SPLIT=0 turns it off): S = 2048, 12 heads of 64:
   // 94 -> 83 us for the whole backward; 8B layer 173 -> 167 us; S = 16384 1006 -> 972 us
@@ -1278,6 +1289,7 @@ at::Tensor flash_bwd(const at::Tensor& dout, const at::Tensor& qk, const at::Ten
 #undef FT_DKDV2
 #undef FT_DQ
   FT_LAUNCH_CHECK();
+  if (direct) return dqkv;
   const long vec = (long)T * ((Hq + 2 * Hkv) * D / 4);
   const int fin_blocks = (int)std::max(1L, std::min((vec + 255) / 256, 4096L));
   hipLaunchKernelGGL(flash_bwd_finalize_kernel, dim3(fin_blocks), block, 0, ft_stream(),
