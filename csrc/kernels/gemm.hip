@@ -124,6 +124,59 @@ __device__ __forceinline__ bf16x8_t frag(const char* img, int r0, int kk, int la
   }
 }
 
+// The same fragment reads issued by inline asm (AR kernels: the one-barrier schedule of the
+// dX / dW layouts). The compiler's waitcnt pass cannot tell a __builtin ds_read_tr (nor, next
+// to it, a ds_read) from the LDS-DMA writes still in flight into the OTHER stage, so it put an
+// s_waitcnt vmcnt(0) in front of the first fragment read of every K-tile: the DMA of tile t+2,
+// issued a quarter-tile earlier, drained there, and the prefetch never overlapped more than
+// one quarter of MFMAs. Reads the pass cannot see get no such wait; the loop waits for them
+// with lgkm_wait<N>() (LDS reads return in order: N = reads issued after the ones needed).
+__device__ __forceinline__ unsigned lds_addr(const char* p) {
+  return (unsigned)(uintptr_t)((const __attribute__((address_space(3))) char*)p);
+}
+
+template <bool KC>
+__device__ __forceinline__ bf16x8_t frag_asm(const char* img, int r0, int kk, int lane) {
+  if constexpr (KC) {
+    const int r = r0 + (lane & 15);
+    const int c = kk * 4 + (lane >> 4);
+    bf16x8_t v;
+    asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(lds_addr(img + r * 128 + ((c ^ (r & 7)) << 4))) : "memory");
+    return v;
+  } else {
+    const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+    const int k = kk * 32 + 8 * g + q;
+    const int u = (r0 >> 3) + (p >> 1);
+    const int half = (p & 1) * 8;
+    bf16x4_t lo, hi;
+    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo) : "v"(lds_addr(img + k * 512 + ((u ^ swz_mn(k)) << 4) + half)) : "memory");
+    asm volatile("ds_read_b64_tr_b16 %0, %1"
+                 : "=v"(hi)
+                 : "v"(lds_addr(img + (k + 4) * 512 + ((u ^ swz_mn(k + 4)) << 4) + half))
+                 : "memory");
+    bf16x8_t r;
+    r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+    r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+    return r;
+  }
+}
+
+template <int N>
+__device__ __forceinline__ void lgkm_wait() {
+  static_assert(N == 0 || N == 4 || N == 8 || N == 12 || N == 15, "lgkm_wait count");
+  if constexpr (N == 0) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  else if constexpr (N == 4) asm volatile("s_waitcnt lgkmcnt(4)" ::: "memory");
+  else if constexpr (N == 8) asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
+  else if constexpr (N == 12) asm volatile("s_waitcnt lgkmcnt(12)" ::: "memory");
+  else asm volatile("s_waitcnt lgkmcnt(15)" ::: "memory");
+}
+
+// keeps the consumers of f after the preceding asm wait
+__device__ __forceinline__ void tie(bf16x8_t (&f)[4]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) asm volatile("" : "+v"(f[i]));
+}
+
 __device__ __forceinline__ float silu(float x) { return x / (1.f + __expf(-x)); }
 
 struct GemmArgs {
@@ -155,7 +208,8 @@ __device__ __forceinline__ void tile_of(int bid, int tiles_m, int tiles_n, int& 
 // 1 no in-loop barrier/wait, 2 no in-loop DMA, 3 no in-loop LDS reads, 4 MFMAs only,
 // 5 no wait for the DMAs before the barrier, 6 the one-barrier-per-tile schedule.
 // (1-5 apply to the two-barrier schedule: the K-contiguous layouts)
-template <bool AK, bool BKC, int EPI, bool RES, int ABL = 0>
+// AR: fragment reads by inline asm with explicit lgkmcnt waits (one-barrier schedule only).
+template <bool AK, bool BKC, int EPI, bool RES, int ABL = 0, bool AR = false>
 __global__ __launch_bounds__(NT, 1) void gemm_kernel(GemmArgs p) {
   __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -239,11 +293,24 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel(GemmArgs p) {
   // tile t+2 overwrites tile t's buffer. Each DMA has a whole K-tile (Q4..Q3) to land.
   bf16x8_t aX[4], aY[4], bX[4], bY[4];
   auto read_a = [&](const char* st, int kk, int mh, bf16x8_t(&af)[4]) {
-    static_for<4>([&](auto I) { af[I] = frag<AK>(st, wr * 128 + (mh * 4 + I) * 16, kk, lane); });
+    static_for<4>([&](auto I) {
+      if constexpr (AR)
+        af[I] = frag_asm<AK>(st, wr * 128 + (mh * 4 + I) * 16, kk, lane);
+      else
+        af[I] = frag<AK>(st, wr * 128 + (mh * 4 + I) * 16, kk, lane);
+    });
   };
   auto read_b = [&](const char* st, int kk, bf16x8_t(&bf)[4]) {
-    static_for<4>([&](auto J) { bf[J] = frag<BKC>(st + OP_BYTES, wc * 64 + J * 16, kk, lane); });
+    static_for<4>([&](auto J) {
+      if constexpr (AR)
+        bf[J] = frag_asm<BKC>(st + OP_BYTES, wc * 64 + J * 16, kk, lane);
+      else
+        bf[J] = frag<BKC>(st + OP_BYTES, wc * 64 + J * 16, kk, lane);
+    });
   };
+  // AR: LDS read instructions per read_a / read_b (a transposed fragment is two reads)
+  constexpr int RA = AK ? 4 : 8, RB = BKC ? 4 : 8;
+  constexpr int RAB = RA + RB > 15 ? 15 : RA + RB;
   auto mma = [&](bf16x8_t(&af)[4], auto MH, bf16x8_t(&bf)[4]) {
     static_for<4>([&](auto I) {
       static_for<4>([&](auto J) {
@@ -269,17 +336,36 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel(GemmArgs p) {
   // transposed-read operand (24 tr-read addresses live) it loses 10-20 %, so dX / dW keep
   // one barrier per K-tile with all DMAs of tile t+2 in Q4.
   constexpr bool ONE_BAR = ABL == 6 || !(AK && BKC);
+  static_assert(!AR || ONE_BAR, "asm reads: one-barrier schedule only");
   if constexpr (ONE_BAR) {
     for (int t = 0; t < nk; ++t) {
       const char* cur = smem + (t & 1) * STAGE_BYTES;
       read_a(cur, 0, 1, aY);
+      if constexpr (AR) {  // aX, bX landed; aY may be in flight
+        lgkm_wait<RA>();
+        tie(aX);
+        tie(bX);
+      }
       mma(aX, H0, bX);
       read_a(cur, 1, 0, aX);
       read_b(cur, 1, bY);
+      if constexpr (AR) {  // aY landed
+        lgkm_wait<RAB>();
+        tie(aY);
+      }
       mma(aY, H1, bX);
       read_a(cur, 1, 1, aY);
+      if constexpr (AR) {  // aX, bY landed
+        lgkm_wait<RA>();
+        tie(aX);
+        tie(bY);
+      }
       mma(aX, H0, bY);
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      if constexpr (AR) {  // aY (and bY) landed at the barrier's wait
+        tie(aY);
+        tie(bY);
+      }
       if (t + 1 < nk) {
         const char* nxt = smem + ((t + 1) & 1) * STAGE_BYTES;
         read_a(nxt, 0, 0, aX);
@@ -590,13 +676,31 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
   *reinterpret_cast<uint4*>(c + m * ldc + n) = pack8(v);
 }
 
+// Fragment reads by inline asm in the one-barrier (dX / dW layout) kernels: 1 (default) or 0
+// (builtin reads; FT_GEMM_ASM_READS / gemm_config, for A/B). See frag_asm.
+int g_asm_reads = [] {
+  const char* e = std::getenv("FT_GEMM_ASM_READS");
+  return e == nullptr ? 1 : std::atoi(e);
+}();
+
 template <bool AK, bool BKC, int EPI>
 void launch(const GemmArgs& a, int splits, hipStream_t s) {
+  const dim3 g(a.tiles_m * a.tiles_n, splits);
   // residual only matters for the bf16 store epilogue (split-K adds it in the reduction)
-  if (EPI == EPI_STORE && a.r != nullptr)
-    hipLaunchKernelGGL((gemm_kernel<AK, BKC, EPI, true>), dim3(a.tiles_m * a.tiles_n, splits), dim3(NT), 0, s, a);
+  const bool res = EPI == EPI_STORE && a.r != nullptr;
+  if constexpr (!(AK && BKC)) {
+    if (g_asm_reads) {
+      if (res)
+        hipLaunchKernelGGL((gemm_kernel<AK, BKC, EPI, true, 0, true>), g, dim3(NT), 0, s, a);
+      else
+        hipLaunchKernelGGL((gemm_kernel<AK, BKC, EPI, false, 0, true>), g, dim3(NT), 0, s, a);
+      return;
+    }
+  }
+  if (res)
+    hipLaunchKernelGGL((gemm_kernel<AK, BKC, EPI, true>), g, dim3(NT), 0, s, a);
   else
-    hipLaunchKernelGGL((gemm_kernel<AK, BKC, EPI, false>), dim3(a.tiles_m * a.tiles_n, splits), dim3(NT), 0, s, a);
+    hipLaunchKernelGGL((gemm_kernel<AK, BKC, EPI, false>), g, dim3(NT), 0, s, a);
 }
 
 int g_tile = 0;     // 0: pick per shape; 128 / 256: force (scripts/gemm_bench.py A/B)
@@ -823,14 +927,15 @@ at::Tensor gemm_ablate(const at::Tensor& a, const at::Tensor& b, int64_t M, int6
   return c;
 }
 
-// A/B hook: tile 0 (per shape) / 128 / 256.
-void gemm_config(int64_t tile) {
+// A/B hook: tile 0 (per shape) / 128 / 256; asm_reads -1 (unchanged) / 0 / 1.
+void gemm_config(int64_t tile, int64_t asm_reads) {
   TORCH_CHECK(tile == 0 || tile == 128 || tile == 256, "gemm_config: tile 0, 128 or 256");
   g_tile = (int)tile;
+  if (asm_reads >= 0) g_asm_reads = (int)asm_reads;
 }
 
 TORCH_LIBRARY_FRAGMENT(ftamd, m) {
-  m.def("gemm_config(int tile) -> ()", &gemm_config);
+  m.def("gemm_config(int tile, int asm_reads=-1) -> ()", &gemm_config);
   m.def("gemm_ablate(Tensor a, Tensor b, int M, int N, int K, int abl) -> Tensor", &gemm_ablate);
   m.def(
       "gemm(Tensor a, bool a_kc, Tensor b, bool b_kc, int M, int N, int K, Tensor(a!)? out, Tensor? residual, "

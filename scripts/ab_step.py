@@ -2,7 +2,9 @@
 """Same-process A/B of step-level knobs on the Llama-3-8B bench step (MI355X).
 
 Knobs toggled between timing windows (alternating rounds, so box and clock drift cancel):
-  gemm  — TunableOp GEMM solution table (tuning/gemm_gfx950.csv) vs the hipBLASLt heuristic
+  hand_dw — weight-gradient GEMMs on the hand-written gfx950 kernel (row-major operands, no
+          transposes) instead of hipBLASLt
+  hand_dx — the dX GEMMs on the hand-written kernel
   dw    — weight-gradient GEMMs on a side stream, concurrent with the dX GEMMs
   sumsq_end — gradient-norm partial sums in one pass after backward instead of during it
   prio  — compute on a high-priority stream (its workgroups dispatch ahead of the side streams')
@@ -33,13 +35,12 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--steps", type=int, default=8)
     ap.add_argument("--rounds", type=int, default=3)
-    ap.add_argument("--knobs", default="gemm,dw")
+    ap.add_argument("--knobs", default="hand_dw,dw")
     a = ap.parse_args()
 
     from fault_tolerant_llm_training_amd.data.synthetic import SyntheticTokens
     from fault_tolerant_llm_training_amd.models.llama import build_model, model_args_for
     from fault_tolerant_llm_training_amd.ops import functional as Fx
-    from fault_tolerant_llm_training_amd.ops import gemm_tuning
     from fault_tolerant_llm_training_amd.optim.adamw import FlatAdamW
     from fault_tolerant_llm_training_amd.parallel.ddp import GradReducer
     from fault_tolerant_llm_training_amd.utils.lr import build_lr_scheduler
@@ -48,7 +49,6 @@ def main():
     torch.cuda.set_device(dev)
     margs = model_args_for(a.model, vocab_size=a.vocab_size, seq_len=a.seq_len)
     model = build_model(margs, dev, torch.bfloat16, seed=1234)
-    print(f"[ab] tuned GEMM table loaded: {gemm_tuning.use_tuned_gemms()}", flush=True)
     red = GradReducer(model.flat, model.sinks_in_backward_order(), bucket_mb=256.0)
     opt = FlatAdamW(model.parameters(), model.flat, lr=5e-5, max_grad_norm=1.0, reducer=red)
     model.gate = opt.gate
@@ -89,7 +89,13 @@ def main():
         torch.cuda.synchronize()
         torch.cuda.set_stream(hp if on else default_stream)
 
-    setters = {"gemm": gemm_tuning.set_enabled, "dw": Fx.set_dw_stream, "tonly": Fx.set_ffn_t_only,
+    def hand(kind):
+        def set_(on):
+            torch.cuda.synchronize()
+            (Fx._HAND_AUTO.add if on else Fx._HAND_AUTO.discard)(kind)
+        return set_
+
+    setters = {"hand_dw": hand("dw"), "hand_dx": hand("dx"), "dw": Fx.set_dw_stream, "tonly": Fx.set_ffn_t_only,
                "dkdv2": kernels().flash_set_dkdv2, "prio": set_prio, "sumsq_end": ddp_mod.set_sumsq_at_end}
     configs = list(itertools.product([False, True], repeat=len(knobs)))
 
