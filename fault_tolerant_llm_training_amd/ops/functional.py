@@ -42,6 +42,25 @@ _GEMM_MODE = os.environ.get("FT_GEMM", "auto")
 _HAND_AUTO = set(k for k in os.environ.get("FT_GEMM_AUTO", "").split(",") if k)
 
 
+def _parse_shapes(spec: str):
+    """"dw:4096x14336x2048,dx:..." -> {("dw", 4096, 14336, 2048), ...} (kind, M, N, K of _hand)."""
+    out = set()
+    for item in (x for x in spec.split(",") if x):
+        kind, dims = item.split(":")
+        m, n, k = (int(v) for v in dims.lower().split("x"))
+        out.add((kind, m, n, k))
+    return out
+
+
+# Individual products the hand kernel takes in "auto" (FT_GEMM_HAND_SHAPES, kind:MxNxK list;
+# "" for none). Default: the Llama-3-8B weight gradient of wo, where the hand kernel (asm
+# fragment reads, row-major dY / X read in place) beats hipBLASLt alone (69.0 vs 72.8 us) and
+# ties it in the step (109.16 vs 109.06 ms, same-process A/B). w2's dW from the SwiGLU
+# kernels' a^T (no transposes at all) measured 0.996x in the step, so it stays opt-in
+# ("dw:4096x14336x2048"); profiles/r2_gemm_hand_dw_wo_w2_ab.log.
+_HAND_SHAPES = _parse_shapes(os.environ.get("FT_GEMM_HAND_SHAPES", "dw:4096x4096x2048"))
+
+
 def set_gemm_mode(mode: str) -> None:
     global _GEMM_MODE
     if mode not in ("auto", "hand", "blas"):
@@ -55,7 +74,7 @@ def _hand(kind: str, M: int, N: int, K: int, *ts) -> bool:
         return False
     if M % 128 or N % 128 or K % 64:  # 256 x 256 tiles where they fill the chip, else 128 x 128
         return False
-    if _GEMM_MODE == "hand" or kind in _HAND_AUTO:
+    if _GEMM_MODE == "hand" or kind in _HAND_AUTO or (kind, M, N, K) in _HAND_SHAPES:
         return True
     # tall-K product with few 256x256 output tiles (the LM head's dX for GPT-2-sized models,
     # [2048 x 768 x 131072]): the hand kernel's split-K fills the chip where hipBLASLt does not
@@ -114,6 +133,17 @@ def weight_grad(dy2: torch.Tensor, x2: torch.Tensor, sink: Optional[GradSink],
         x2 = xT.t()
     T, N = dy2.shape
     K = x2.shape[1]
+    if xT is not None and dyT is None and _hand("dw", N, K, T, dy2, xT) and dy2.is_contiguous() \
+            and xT.is_contiguous():
+        # dW[N, K] = dY^T X with X given transposed (the SwiGLU kernels' a^T [K, T]): the hand
+        # kernel reads dY [T, N] as A^T and X^T as a K-contiguous B — no transposes at all
+        out = sink.buf.view(N, K) if sink is not None else None
+        acc = sink.accumulate if sink is not None else False
+        r = kernels().gemm(dy2, False, xT, True, N, K, T, out, None, acc, 0)
+        if sink is not None:
+            sink.ready()
+            return None
+        return r
     if _hand("dw", N, K, T, dy2, x2) and dy2.is_contiguous() and x2.is_contiguous():
         # dW[N, K] = dY^T X read straight from the row-major dY [T, N] and X [T, K]
         out = sink.buf.view(N, K) if sink is not None else None

@@ -5,6 +5,7 @@ Knobs toggled between timing windows (alternating rounds, so box and clock drift
   hand_dw — weight-gradient GEMMs on the hand-written gfx950 kernel (row-major operands, no
           transposes) instead of hipBLASLt
   hand_dx — the dX GEMMs on the hand-written kernel
+  hand_dw_wo_w2 / hand_dw_wo — only those weight gradients on the hand-written kernel
   dw    — weight-gradient GEMMs on a side stream, concurrent with the dX GEMMs
   sumsq_end — gradient-norm partial sums in one pass after backward instead of during it
   prio  — compute on a high-priority stream (its workgroups dispatch ahead of the side streams')
@@ -95,7 +96,19 @@ def main():
             (Fx._HAND_AUTO.add if on else Fx._HAND_AUTO.discard)(kind)
         return set_
 
-    setters = {"hand_dw": hand("dw"), "hand_dx": hand("dx"), "dw": Fx.set_dw_stream, "tonly": Fx.set_ffn_t_only,
+    def shapes(spec):
+        sh = Fx._parse_shapes(spec)
+
+        def set_(on):
+            torch.cuda.synchronize()
+            for x in sh:
+                (Fx._HAND_SHAPES.add if on else Fx._HAND_SHAPES.discard)(x)
+        return set_
+
+    setters = {"hand_dw": hand("dw"), "hand_dx": hand("dx"),
+               # Llama-3-8B dW of wo and w2 (the products where the hand kernel >= hipBLASLt alone)
+               "hand_dw_wo_w2": shapes("dw:4096x4096x2048,dw:4096x14336x2048"),
+               "hand_dw_wo": shapes("dw:4096x4096x2048"), "dw": Fx.set_dw_stream, "tonly": Fx.set_ffn_t_only,
                "dkdv2": kernels().flash_set_dkdv2, "prio": set_prio, "sumsq_end": ddp_mod.set_sumsq_at_end}
     configs = list(itertools.product([False, True], repeat=len(knobs)))
 

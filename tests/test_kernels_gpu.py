@@ -282,6 +282,31 @@ def test_weight_grad_layouts(mode, monkeypatch):
     assert rel(dw, ref) < 1e-2
 
 
+@pytest.mark.parametrize("given_t", [False, True])
+def test_weight_grad_hand_shapes(given_t, monkeypatch):
+    """A product listed in _HAND_SHAPES runs on the hand GEMM (asm-read dW kernel), from the
+    row-major X or from X^T (the SwiGLU kernels' a^T), into a sink with accumulation."""
+    from fault_tolerant_llm_training_amd.ops import functional as Fx
+    from fault_tolerant_llm_training_amd.ops.grad_sink import GradSink
+
+    T, N, Kd = 512, 256, 768
+    monkeypatch.setattr(Fx, "_HAND_SHAPES", {("dw", N, Kd, T)})
+    dy = torch.randn(T, N, device="cuda").bfloat16()
+    x = torch.randn(T, Kd, device="cuda").bfloat16()
+    ref = dy.float().t() @ x.float()
+    dw = Fx.weight_grad(dy, None, None, xT=x.t().contiguous()) if given_t else Fx.weight_grad(dy, x, None)
+    assert rel(dw, ref) < 1e-2
+    buf = torch.randn(N * Kd, device="cuda").bfloat16()
+    base = buf.float().clone()
+    sink = GradSink(buf)
+    sink.accumulate = True
+    if given_t:
+        Fx.weight_grad(dy, None, sink, xT=x.t().contiguous())
+    else:
+        Fx.weight_grad(dy, x, sink)
+    assert rel(buf.view(N, Kd), base.view(N, Kd) + ref) < 1e-2
+
+
 @pytest.mark.parametrize("ln", [False, True])
 def test_add_norm_fused(ln):
     """AddNormFn on the GPU (fused residual add + norm, norm bwd with the residual grad fused)
