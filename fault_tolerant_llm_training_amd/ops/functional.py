@@ -34,11 +34,12 @@ IGNORE_INDEX = -100
 # below, from scripts/gemm_bench.py on MI355X), "hand" (every fitting shape), "blas" (none).
 _GEMM_MODE = os.environ.get("FT_GEMM", "auto")
 # products the hand kernel takes in "auto" (FT_GEMM_AUTO, comma list of fwd,dx,dw,ffn).
-# Default: none. Measured on the Llama-3-8B step (profiles/r2_gemm_hand_vs_hipblaslt.md): the
-# hand kernel runs each product at 0.72-0.95x of hipBLASLt, and the whole step at 109.4 ms
-# (all hipBLASLt) vs 112.9 (SwiGLU-fused FFN on the hand kernel), 113.7 (dW), 118.8 (both),
-# 123.1 (every product) — the transposes and SwiGLU passes it removes cost less than the GEMM
-# speed it gives up.
+# Default: none. Measured on the Llama-3-8B step (profiles/r2_gemm_hand_vs_hipblaslt.md,
+# profiles/r2_gemm_asm_reads_ab.log): the hand kernel runs the products at 0.56-1.06x of
+# hipBLASLt, and the whole step at 109.4 ms (all hipBLASLt) vs 112.9 (SwiGLU-fused FFN on the
+# hand kernel), 118.8 (FFN + dW), 123.1 (every product); after the asm-read fix, hand dX 0.989x
+# and hand dW 0.963x of the all-hipBLASLt step — the transposes and SwiGLU passes it removes
+# cost less than the GEMM speed it gives up.
 _HAND_AUTO = set(k for k in os.environ.get("FT_GEMM_AUTO", "").split(",") if k)
 
 
