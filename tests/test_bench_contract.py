@@ -92,3 +92,22 @@ def test_bench_grad_accum_two_ranks():  # (no checkpoint block: --no-ckpt)
     j = _json_lines(r.stdout)[0]
     assert j["config"]["global_batch"] == 4 and j["grad_accum"] == 2
     assert abs(j["value"] - 4 * 64 / (j["ms_per_step"] / 1e3)) / j["value"] < 0.02
+
+
+@pytest.mark.parametrize("world", [4, 8])
+def test_bench_torchrun_n_ranks_zero1(world, tmp_path):
+    """Rehearsal of the driver's N = 4 / 8 runs (one process per GPU there; gloo ranks here): the
+    default ZeRO-1 mode with 64-element-aligned shards, the sparse embedding exchange across all
+    ranks, the exposed-communication re-timing and the sharded checkpoint block."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", str(world)] + ARGS
+    r = subprocess.run(cmd, cwd=ROOT, env=_env(tmp_path), capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1, r.stdout
+    j = lines[0]
+    assert j["n_gpus"] == world and j["config"]["parallelism"] == f"dp{world}"
+    assert j["config"]["global_batch"] == world and j["grad_mode"] == "zero1"
+    assert abs(j["value"] - world * 64 / (j["ms_per_step"] / 1e3)) / j["value"] < 0.02
+    assert "exposed_comm_ms_per_step" in j and j["comm_GB_per_rank_per_step"] >= 0
+    _check_ckpt(j, world)

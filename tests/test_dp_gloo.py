@@ -67,7 +67,8 @@ def _worker(rank, world, port, out_dir, bucket_mb, mode):
 
 
 @pytest.mark.parametrize("mode,bucket_mb,world", [("allreduce", 0.05, 2), ("allreduce", 256.0, 2), ("zero1", 0.05, 2),
-                                                   ("zero1", 256.0, 2), ("zero1", 0.05, 4), ("allreduce", 0.05, 4)])
+                                                   ("zero1", 256.0, 2), ("zero1", 0.05, 4), ("allreduce", 0.05, 4),
+                                                   ("zero1", 0.05, 8)])
 def test_ddp_grads_equal_single_process_global_batch(tmp_path, mode, bucket_mb, world):
     mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path), bucket_mb, mode), nprocs=world,
                        start_method="spawn")
