@@ -148,7 +148,12 @@ class GradReducer:
         # embedding gradient; its bucket needs no collective.
         emb = "tok_embeddings.weight"
         self.sparse_embedding = (sparse_embedding and self.world > 1 and mode != "local" and emb in flat.slots)
-        self.buckets = make_buckets(flat, bucket_mb, solo=(emb,) if self.sparse_embedding else ())
+        # The token-embedding table in a bucket of its own on one GPU too, so the next forward
+        # (which needs it first) waits only for the table's AdamW, not for the layers bucketed
+        # with it: GPT-2-medium 15.07 -> 14.97 ms/step, GPT-2-small and 8B unchanged
+        # (profiles/r2_emb_solo_bucket_ab.log; FT_EMB_SOLO_BUCKET=0 restores the plain cut)
+        solo_emb = self.sparse_embedding or (os.environ.get("FT_EMB_SOLO_BUCKET", "1") == "1" and emb in flat.slots)
+        self.buckets = make_buckets(flat, bucket_mb, solo=(emb,) if solo_emb else ())
         if self.sparse_embedding:
             es = flat.slots[emb]
             for b in self.buckets:
