@@ -903,9 +903,10 @@ __global__ __launch_bounds__(64 * NW * SPLIT, SPLIT == 1 ? 4 / NW : 8 / (NW * SP
   constexpr int TILE = BN * D * 2;
   // K | V tiles arrive by LDS-DMA (no staging VGPRs held across the compute: at one wave
   // per SIMD the register-staged prefetch pushed the dQ accumulators through AGPR copies
-  // every tile). Two separate LDS objects + a loop unrolled by two: every LDS read names
-  // a buffer the in-flight DMA provably does not write, so the compiler never drains the
-  // prefetch before reading the current tile.
+  // every tile). Two separate LDS objects + a loop unrolled by two: every row read names a
+  // buffer the in-flight DMA provably does not write, so the compiler does not drain the
+  // prefetch before them (it still does before the first transposed ds_read_b64_tr_b16 of a
+  // tile; asm reads that avoid it measured no gain: profiles/r2_flash_d64_forward_ab.log).
   __shared__ __attribute__((aligned(16))) char kv0[2 * TILE * SPLIT];
   __shared__ __attribute__((aligned(16))) char kv1[2 * TILE * SPLIT];
 
