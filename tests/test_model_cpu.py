@@ -151,3 +151,22 @@ def test_selective_checkpointing_skips_attention_recompute(monkeypatch):
         assert len(calls) == per_step + a.n_layers
         assert torch.allclose(m.flat.grads, ref.flat.grads, rtol=0, atol=1e-6)
         assert all(l.attn_keep.o is None for l in m.layers.values()) or recompute_attention
+
+
+@pytest.mark.parametrize("solo", ["1", "0"])
+def test_embedding_solo_bucket_on_one_rank(solo, monkeypatch):
+    """On one rank the token-embedding table gets an optimizer bucket of its own (the next forward
+    waits only for the table's AdamW); FT_EMB_SOLO_BUCKET=0 restores the plain size cut. Either
+    way the buckets tile the flat buffer exactly."""
+    from fault_tolerant_llm_training_amd.models.llama import build_model, model_args_for
+    from fault_tolerant_llm_training_amd.parallel.ddp import GradReducer
+
+    monkeypatch.setenv("FT_EMB_SOLO_BUCKET", solo)
+    m = build_model(model_args_for("tiny", vocab_size=512, seq_len=32), "cpu", torch.bfloat16, seed=0)
+    red = GradReducer(m.flat, m.sinks_in_backward_order(), bucket_mb=1.0)
+    spans = sorted((b.lo, b.hi) for b in red.buckets)
+    assert spans[0][0] == 0 and spans[-1][1] == m.flat.numel
+    assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+    es = m.flat.slots["tok_embeddings.weight"]
+    own = any(b.lo == es.offset and b.hi == es.offset + es.numel for b in red.buckets)
+    assert own == (solo == "1")
