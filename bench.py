@@ -198,6 +198,9 @@ def main():
         "dtype": "bf16",
         "data": "synthetic",
         "config": {"model": a.model, "global_batch": B * K * world, "seq_len": S, "parallelism": f"dp{world}"},
+        # the metric is named per GPU; `value` is the driver's whole-job aggregate: both explicit
+        "value_basis": "whole job: tokens/s summed over all n_gpus (per GPU: tokens_per_s_per_gpu)",
+        "tokens_per_s_whole_job": round(tok_s, 1),
         "tokens_per_s_per_gpu": round(tok_s / world, 1),
         "mfu_vs_2.5PF_dense": round(mfu, 4),
         "final_loss": round(final_loss, 4),

@@ -7,6 +7,15 @@
 // distinct token sums its dy rows in fp32 and writes the bf16 gradient row
 // straight into the flat gradient buffer. Rows never touched are zeroed by a
 // memset of the embedding's gradient slice.
+//
+// The sort is in-tree (no ATen/rocPRIM kernel on the path): one 1024-thread workgroup
+// runs a stable LSD radix sort with 6-bit digits (3 passes for a 131072-token vocabulary)
+// over the B*S token ids (2048 per GPU; 16384 after the DP sparse exchange gathers 8
+// ranks). Per pass: a digit histogram (LDS atomics: counts are order-independent),
+// then rounds of 1024 keys in index order; inside a wave, lanes with the same digit find
+// each other with six ballots and rank themselves by lane (popcount of the lower lanes'
+// match mask), wave counts are prefix-summed across the 16 waves per digit, and every key
+// goes to bin start + earlier rounds + earlier waves + its rank — i.e. stably.
 #include "torch_utils.h"
 
 namespace {
@@ -21,16 +30,86 @@ __global__ __launch_bounds__(256) void emb_fwd_kernel(const int64_t* __restrict_
   for (int c = threadIdx.x; c < D / 8; c += blockDim.x) dst[c] = src[c];
 }
 
+constexpr int SORT_NT = 1024, SORT_W = SORT_NT / 64, SORT_BITS = 6, SORT_BINS = 1 << SORT_BITS;
+
+// Stable LSD radix sort of tok[0..T) (values < 2^(6*passes)) with the row index as payload.
+// Pass p reads (p == 0 ? tok, iota : buffer (p-1)&1) and writes buffer p&1 (k[2][T], v[2][T]).
+__global__ __launch_bounds__(SORT_NT) void tok_sort_kernel(const int64_t* __restrict__ tok, int T, int passes,
+                                                           int* __restrict__ keys, int* __restrict__ vals) {
+  __shared__ int hist[SORT_BINS];
+  __shared__ int start[SORT_BINS];
+  __shared__ int rbase[SORT_BINS];
+  __shared__ int wcnt[SORT_W][SORT_BINS];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const unsigned long long lower = (1ull << lane) - 1ull;
+  for (int pass = 0; pass < passes; ++pass) {
+    const int shift = pass * SORT_BITS;
+    const int* sk = pass == 0 ? nullptr : keys + ((pass - 1) & 1) * (long)T;
+    const int* sv = pass == 0 ? nullptr : vals + ((pass - 1) & 1) * (long)T;
+    int* dk = keys + (pass & 1) * (long)T;
+    int* dv = vals + (pass & 1) * (long)T;
+    if (tid < SORT_BINS) hist[tid] = 0;
+    __syncthreads();
+    for (int i = tid; i < T; i += SORT_NT) {
+      const int k = sk ? sk[i] : (int)tok[i];
+      atomicAdd(&hist[(k >> shift) & (SORT_BINS - 1)], 1);
+    }
+    __syncthreads();
+    if (tid == 0) {
+      int s = 0;
+      for (int b = 0; b < SORT_BINS; ++b) {
+        start[b] = s;
+        s += hist[b];
+      }
+    }
+    for (int base = 0; base < T; base += SORT_NT) {
+      const int i = base + tid;
+      const bool valid = i < T;
+      const int k = valid ? (sk ? sk[i] : (int)tok[i]) : 0;
+      const int v = valid ? (sk ? sv[i] : i) : 0;
+      const int d = (k >> shift) & (SORT_BINS - 1);
+      unsigned long long m = __ballot(valid);
+#pragma unroll
+      for (int b = 0; b < SORT_BITS; ++b) {
+        const unsigned long long bb = __ballot(valid && ((d >> b) & 1));
+        m &= ((d >> b) & 1) ? bb : ~bb;
+      }
+      const int rank = __popcll(m & lower);
+      wcnt[wid][lane] = 0;
+      __syncthreads();
+      if (valid && rank == 0) wcnt[wid][d] = __popcll(m);
+      __syncthreads();
+      if (tid < SORT_BINS) {  // exclusive prefix over the waves, per digit
+        int s = 0;
+        for (int w = 0; w < SORT_W; ++w) {
+          const int c = wcnt[w][tid];
+          wcnt[w][tid] = s;
+          s += c;
+        }
+        rbase[tid] = start[tid];
+        start[tid] += s;
+      }
+      __syncthreads();
+      if (valid) {
+        const int pos = rbase[d] + wcnt[wid][d] + rank;
+        dk[pos] = k;
+        dv[pos] = v;
+      }
+      __syncthreads();  // (also orders this pass's global writes before the next pass's reads)
+    }
+  }
+}
+
 // sorted_tok[i], perm[i]: i-th smallest token and its original row.
-__global__ __launch_bounds__(256) void emb_bwd_kernel(const int64_t* __restrict__ sorted_tok,
-                                                      const int64_t* __restrict__ perm,
+__global__ __launch_bounds__(256) void emb_bwd_kernel(const int* __restrict__ sorted_tok,
+                                                      const int* __restrict__ perm,
                                                       const bf16_t* __restrict__ dy,
                                                       bf16_t* __restrict__ dw, int T, int D,
                                                       bool accumulate) {
   const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
   if (wave >= T) return;
-  const int64_t t = sorted_tok[wave];
+  const int t = sorted_tok[wave];
   if (wave > 0 && sorted_tok[wave - 1] == t) return;  // not the segment head
   int end = wave + 1;
   while (end < T && sorted_tok[end] == t) ++end;
@@ -86,16 +165,25 @@ void embedding_bwd_(const at::Tensor& dy, const at::Tensor& tokens, const at::Te
   const int T = tokens.numel();
   TORCH_CHECK(dy.numel() == (long)T * D, "embedding_bwd: shape mismatch");
   const at::DeviceGuard guard(dw.device());
-  auto flat = tokens.reshape({-1});
-  auto sorted = at::sort(flat, /*stable=*/true, /*dim=*/0, /*descending=*/false);
-  auto sorted_tok = std::get<0>(sorted).contiguous();
-  auto perm = std::get<1>(sorted).contiguous();
+  TORCH_CHECK(tokens.scalar_type() == at::kLong, "embedding_bwd: tokens must be int64");
+  const long V = dw.size(0);
+  TORCH_CHECK(V >= 1 && V < (1L << 30), "embedding_bwd: vocabulary size out of range");
+  int bits = 1;
+  while ((1L << bits) < V) ++bits;
+  const int passes = (bits + SORT_BITS - 1) / SORT_BITS;
+  auto flat = tokens.reshape({-1}).contiguous();
   if (!accumulate) FT_HIP_CHECK(hipMemsetAsync(dw.data_ptr(), 0, dw.nbytes(), ft_stream()));
   if (T > 0) {
+    auto kv = at::empty({4, (long)T}, tokens.options().dtype(at::kInt));  // keys[2][T], vals[2][T]
+    int* keys = mptr<int>(kv);
+    int* vals = keys + 2L * T;
+    hipLaunchKernelGGL(tok_sort_kernel, dim3(1), dim3(SORT_NT), 0, ft_stream(), cptr<int64_t>(flat), T, passes,
+                       keys, vals);
+    FT_LAUNCH_CHECK();
+    const long fin = (long)((passes - 1) & 1) * T;
     const int blocks = (T * 64 + 255) / 256;
-    hipLaunchKernelGGL(emb_bwd_kernel, dim3(blocks), dim3(256), 0, ft_stream(),
-                       cptr<int64_t>(sorted_tok), cptr<int64_t>(perm), cptr<bf16_t>(dy),
-                       mptr<bf16_t>(dw), T, D, accumulate);
+    hipLaunchKernelGGL(emb_bwd_kernel, dim3(blocks), dim3(256), 0, ft_stream(), keys + fin, vals + fin,
+                       cptr<bf16_t>(dy), mptr<bf16_t>(dw), T, D, accumulate);
   }
   FT_LAUNCH_CHECK();
 }

@@ -14,8 +14,8 @@ from .._native import kernels
 
 # Backward variant: 1 = deterministic (default): KV-major dK/dV kernel + Q-major dQ
 # kernel, no atomics, bit-reproducible — GPU resume is bit-exact with it and it runs
-# as fast as 0 = dQ accumulated with fp32 atomics in the KV-major kernel (330 vs 335 us
-# on the Llama-3-8B layer shape, profiles/r1_flash_bench.log).
+# as fast as 0 = dQ accumulated with fp32 atomics in the KV-major kernel (Llama-3-8B
+# layer shape: profiles/r1_flash_kernels.md).
 _BWD_MODE = int(os.environ.get("FT_FLASH_BWD_MODE", "1"))
 
 

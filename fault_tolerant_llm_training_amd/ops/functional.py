@@ -668,7 +668,8 @@ def feed_forward(x, w13, w2, sink13=None, sink2=None):
     if x.is_cuda and _FUSED_FFN:
         T, D = x.numel() // x.shape[-1], x.shape[-1]
         F = w13.shape[0] // 2
-        if _hand("ffn", T, 2 * F, D, x, w13, w2) and F % 256 == 0:
+        # gemm_swiglu / gemm_swiglu_bwd tile T and F by 256 (BM / BN of the 256 kernel)
+        if _hand("ffn", T, 2 * F, D, x, w13, w2) and F % 256 == 0 and T % 256 == 0:
             return FusedFFNFn.apply(x, w13, w2, sink13, sink2)
         if w13.shape[0] % 128 == 0 and T % 64 == 0:
             return FeedForwardFn.apply(x, w13, w2, sink13, sink2)

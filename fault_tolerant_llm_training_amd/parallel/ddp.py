@@ -75,7 +75,7 @@ def set_sumsq_at_end(on: bool) -> None:
 
 class Bucket:
     __slots__ = ("idx", "lo", "hi", "needed", "filled", "launched", "work", "part_lo", "part_hi",
-                 "shard_lo", "shard_len", "event", "sparse")
+                 "shard_lo", "shard_len", "event", "sparse", "post")
 
     def __init__(self, idx, lo, hi, needed):
         self.idx, self.lo, self.hi, self.needed = idx, lo, hi, needed
@@ -87,6 +87,7 @@ class Bucket:
         self.shard_len = 0    # elements per rank
         self.event = None
         self.sparse = False   # reduced by the sparse embedding exchange, not a bucket collective
+        self.post = None      # fp32 reduce: copies the reduced fp32 result back (after work.wait())
 
     @property
     def numel(self):
@@ -123,7 +124,14 @@ def make_buckets(flat: FlatParamSpace, bucket_mb: float, solo=()) -> List[Bucket
 class GradReducer:
     def __init__(self, flat: FlatParamSpace, extra_sinks: List[GradSink], bucket_mb: float = 256.0,
                  mode: Optional[str] = None, group=None, overlap: Optional[bool] = None,
-                 sparse_embedding: bool = True):
+                 sparse_embedding: bool = True, reduce_dtype: str = "native"):
+        """``reduce_dtype``: "native" (or "bf16") reduces the gradient buckets in their own
+        dtype — RCCL adds in fp32 per hop and rounds to bf16 (tests/test_dp_bf16_numerics.py
+        bounds the result); "fp32" (opt-in, ``--dp-reduce-dtype fp32``) reduces an fp32 copy
+        of each bucket (2x the bytes on the links) and rounds once at the end."""
+        if reduce_dtype not in ("native", "bf16", "fp32"):
+            raise ValueError(f"reduce_dtype {reduce_dtype!r}")
+        self.reduce_fp32 = reduce_dtype == "fp32" and flat.grads.dtype != torch.float32
         self.flat = flat
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
@@ -297,6 +305,17 @@ class GradReducer:
         grads = self.flat.grads[b.lo : b.hi]
         if b.sparse or self.dry_comm:
             pass  # sparse: summed by the embedding exchange inside the embedding backward
+        elif self.reduce_fp32:
+            src = grads.float()
+            if self.mode == "allreduce":
+                b.work = dist.all_reduce(src, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+                b.post = lambda: grads.copy_(src)
+            else:
+                out = src.new_empty(b.shard_len)
+                b.work = dist.reduce_scatter_tensor(out, src, op=dist.ReduceOp.SUM, group=self.group,
+                                                    async_op=True)
+                shard = self.grad_shard(b)
+                b.post = lambda: shard.copy_(out)
         elif self.mode == "allreduce":
             b.work = dist.all_reduce(grads, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
         elif self.mode == "zero1":
@@ -312,10 +331,17 @@ class GradReducer:
             if b.work is not None:
                 b.work.wait()  # side stream waits for the collective (host does not)
                 b.work = None
+                self._post(b)
             if SUMSQ_AT_END:
                 self._pending_sumsq.append(b)
             else:
                 self._sumsq(self.grad_for_update(b), b)
+
+    @staticmethod
+    def _post(b: Bucket) -> None:
+        if b.post is not None:
+            b.post()
+            b.post = None
 
     def finish(self) -> None:
         """Launch stragglers; after this, ``partials`` hold every bucket's sum of squares
@@ -338,6 +364,7 @@ class GradReducer:
                 if b.work is not None:
                     b.work.wait()
                     b.work = None
+                    self._post(b)
                 self._sumsq(self.grad_for_update(b), b)
         for b in self.buckets:
             b.filled = 0

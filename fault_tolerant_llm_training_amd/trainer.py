@@ -53,6 +53,7 @@ from .utils.lr import build_lr_scheduler, rollback_lr_scheduler
 
 SIGTERM_NUM = int(signal.SIGTERM)
 SYNTHETIC_VOCAB = 131072  # the reference's Mistral-Nemo tokenizer size
+DP_DEFAULT_SAVE_EVERY = 200  # --save-every when unset and world > 1 (BASELINE config 3)
 
 
 class InjectedFault(Exception):
@@ -268,7 +269,7 @@ def train(args) -> int:
 
     state_dtype = PRECISION_STR_TO_DTYPE[args.optimizer_state_dtype] if args.optimizer_state_dtype else None
     reducer = GradReducer(model.flat, model.sinks_in_backward_order(), bucket_mb=args.dp_bucket_mb,
-                          mode=args.dp_mode or None)
+                          mode=args.dp_mode or None, reduce_dtype=args.dp_reduce_dtype)
     optimizer = FlatAdamW(model.parameters(), model.flat, lr=args.learning_rate, state_dtype=state_dtype,
                           max_grad_norm=args.grad_max_norm, fused=args.fused_optimizer, reducer=reducer)
     model.gate = optimizer.gate
@@ -306,6 +307,18 @@ def train(args) -> int:
 
     ckpt_path = checkpoint_file(args.checkpoint_path, job_id)
     ckpt = {"engine": None}
+    # periodic saves: on by default under data parallelism (BASELINE config 3 cadence), so a
+    # lost rank (OOM-kill, node failure) costs at most that many steps — ZeRO-1 survivors
+    # cannot write its optimizer shards (reference train.py:121-129 saves on every path it sees)
+    save_every = args.save_every if args.save_every >= 0 else (DP_DEFAULT_SAVE_EVERY if info.world_size > 1 else 0)
+    if save_every and info.world_size > 1:
+        logger.info(f"Periodic checkpoint every {save_every} steps")
+    durable = {"step": None, "path": None}  # last checkpoint known to be on disk (this job)
+    if info.is_main:
+        try:  # a previous job's peer-loss lock (same job id on requeue) would block the next solo save
+            os.unlink(ckpt_path + ".solo")
+        except FileNotFoundError:
+            pass
     # FT_SHARDED_CKPT=1 forces the multi-writer protocol on a 1-rank process group (test hook)
     sharded = info.world_size > 1 or (info.ckpt_group is not None and os.environ.get("FT_SHARDED_CKPT") == "1")
 
@@ -395,6 +408,7 @@ def train(args) -> int:
         a0, a1 = (int(v) for v in args.profile_steps.split(":"))
         prof_range = (a0, a1)
     fault = _RankFault(os.environ.get("FT_INJECT_FAULT", ""), info.rank)
+    last_save_step = training_step  # a resumed run does not re-save the state it just loaded
     # optimizer step k <-> training step k - offset (0 for fresh runs; resumed runs load both)
     offset = optimizer.step_count - training_step
     pending_err: Optional[BaseException] = None  # this rank's mid-step failure (step completed poisoned)
@@ -413,13 +427,19 @@ def train(args) -> int:
         losslog.drop_after(training_step)
         return training_step
 
-    def boundary(final: bool = False) -> None:
+    def boundary(final: bool = False, save_due: bool = False) -> None:
         """Step boundary: one vote over every rank (signal, local error, lagged non-finite check,
-        token count of the next batch, losses to log), then either go on or stop together."""
+        token count of the next batch, losses to log), then either go on or stop together.
+
+        ``save_due``: a periodic checkpoint follows if the vote passes. Its non-finite check
+        then covers every optimizer step so far (blocking), so the file never records steps
+        whose updates the device guard skipped."""
         nonlocal pending_err
+        if save_due:
+            complete_pending()  # graph mode: the snapshot needs the last step's optimizer update
         sig = monitor.pending()
         err = 1.0 if pending_err is not None else 0.0
-        upto = optimizer.step_count if final else optimizer.step_count - 1
+        upto = optimizer.step_count if (final or save_due) else optimizer.step_count - 1
         bad = optimizer.first_nonfinite(upto=upto, block=True)
         entries = losslog.take(training_step - (0 if final else 2))
         vec = [float(sig), err, float(bad or 0), float(boundary.count)] + [e[1][0] for e in entries]
@@ -496,9 +516,16 @@ def train(args) -> int:
                 if pending_err is None:
                     pending_err = e
             boundary.count = float(batch.num_items) if batch is not None else 0.0
-            boundary()
+            # the periodic save is decided from the agreed step alone and taken only after the
+            # vote passed on every rank: a rank that failed in the previous step stops all of
+            # them at the vote instead of leaving its peers inside the save's collectives
+            save_due = bool(save_every) and training_step % save_every == 0 and training_step != last_save_step
+            boundary(save_due=save_due)
             if batch is None:  # unreachable: a local error always stops every rank above
                 raise RuntimeError("no batch")
+            if save_due:
+                save_checkpoint(blocking=args.no_async_checkpoint, step_now=training_step)
+                last_save_step = training_step
 
             if prof_range is not None and training_step == prof_range[0] and prof is None:
                 acts = [torch.profiler.ProfilerActivity.CPU]
@@ -564,7 +591,8 @@ def train(args) -> int:
                 pending_err = e
                 reducer.fault_after_buckets = 0
                 try:
-                    _complete_step(phase, reducer, optimizer, lr_scheduler, (K * B, S), emb_dim)
+                    _complete_step(phase, reducer, optimizer, lr_scheduler, (K * B, S), emb_dim,
+                                   fence=ckpt["engine"].fence if ckpt["engine"] is not None else None)
                 except Exception as e2:  # noqa: BLE001
                     raise _FatalStepError(f"could not complete step {training_step} after {e!r}: {e2!r}") from e2
                 lr_now = optimizer.param_groups[0]["lr"]
@@ -591,10 +619,6 @@ def train(args) -> int:
                 prof.export_chrome_trace(out)
                 logger.info(f"torch.profiler trace written to {out}")
                 prof, prof_range = None, None
-            if (pending_err is None and args.save_every and training_step % args.save_every == 0
-                    and training_step < args.training_steps):
-                complete_pending()  # graph mode: the snapshot needs this step's optimizer update
-                save_checkpoint(blocking=args.no_async_checkpoint, step_now=training_step)
         complete_pending()
         boundary.count = 0.0
         boundary(final=True)  # drains the loss log, last non-finite check, last signals
@@ -629,6 +653,19 @@ def train(args) -> int:
         # on collectives that will never complete).
         logger.error(f"[EXIT HANDLER] Lost a peer rank: {e}")
         step_now = training_step
+        if ckpt["engine"] is not None:
+            try:  # a save already published by every rank counts; one stuck on the dead peer does not
+                ckpt["engine"].poll()
+            except Exception:  # noqa: BLE001
+                pass
+            ok = [h for h in ckpt["engine"].history if not h.error]
+            if ok:
+                durable.update(step=ok[-1].step, path=ok[-1].path)
+        if durable["step"] is not None:
+            logger.error(f"[EXIT HANDLER] Last durable checkpoint: {durable['path']} at step {durable['step']} "
+                         f"(resume with --checkpoint-id {job_id})")
+        else:
+            logger.error("[EXIT HANDLER] No durable checkpoint was written by this job")
         complete = isinstance(e, fdist.PeerFailure) and pending_err is None
         if complete and info.distributed and device.type == "cuda" and not _drained(device, 0.5 * info.peer_timeout_s):
             logger.error("[EXIT HANDLER] the last step's collectives never completed; no complete state to save")
@@ -671,17 +708,21 @@ def _drained(device: torch.device, timeout_s: float) -> bool:
     return not t.is_alive()
 
 
-def _complete_step(phase: str, reducer, optimizer, lr_scheduler, tokens_shape, dim: int) -> None:
+def _complete_step(phase: str, reducer, optimizer, lr_scheduler, tokens_shape, dim: int, fence=None) -> None:
     """After a failure at ``phase``, finish this rank's share of the step so the peers'
     collectives complete: unlaunched buckets go out poisoned (NaN), so every rank's
     non-finite guard skips the step's update; then the optimizer/scheduler steps run as
     on the peers. Failures before backward's last bucket poison the whole step; a
-    failure after ``optimizer.step()`` was enqueued leaves a valid, complete step."""
+    failure after ``optimizer.step()`` was enqueued leaves a valid, complete step.
+    ``fence``: the checkpoint engine's snapshot fence — an async periodic snapshot still
+    copying the state must finish before this optimizer step writes it (as in the loop)."""
     if phase in ("forward", "backward", "finish", "optimizer"):
         # at "optimizer" the gradients are complete and every bucket went out with valid
         # data: the peers' step is valid, so this rank takes the same valid step
         if phase != "optimizer":
             reducer.poison_and_complete(tokens_shape, dim)
+        if fence is not None:
+            fence()
         optimizer.step()
         lr_scheduler.step()
     elif phase == "step":

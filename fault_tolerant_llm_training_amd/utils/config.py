@@ -121,8 +121,9 @@ def build_parser() -> argparse.ArgumentParser:
     parser.add_argument(
         "--save-every",
         type=int,
-        default=0,
-        help="Periodic asynchronous checkpoint every N steps (0 disables)",
+        default=-1,
+        help="Periodic asynchronous checkpoint every N steps (0 disables; default: 200 under data "
+        "parallelism, so a lost rank costs at most that many steps, else 0)",
     )
     parser.add_argument(
         "--no-async-checkpoint",
@@ -168,11 +169,13 @@ def build_parser() -> argparse.ArgumentParser:
         help="Data-parallel gradient mode (default zero1: reduce-scatter + sharded AdamW + all-gather)",
     )
     parser.add_argument(
-        "--consensus-every",
-        type=int,
-        default=1,
-        help="(kept for compatibility) the ranks now vote at every step boundary: signals, rank-local "
-        "errors and non-finite gradients must stop every rank at the same step",
+        "--dp-reduce-dtype",
+        type=str,
+        default="native",
+        choices=["native", "fp32"],
+        help="Data-parallel gradient reduction dtype: native (the gradient dtype, bf16 by default; the "
+        "error bound is in docs/PERFORMANCE.md) or fp32 (reduce an fp32 copy of each bucket: 2x the "
+        "bytes on the links, one rounding)",
     )
     parser.add_argument(
         "--grad-accum",

@@ -202,3 +202,63 @@ def test_hung_rank_detected_after_peer_timeout(tmp_path):
     assert rc0 == 1, logs[0]
     assert "Lost a peer rank" in logs[0]
     assert waited < 60, waited
+
+
+@pytest.mark.parametrize("phase,saved", [("forward", 3), ("post", 4)])
+def test_fault_just_before_periodic_save_boundary(tmp_path, phase, saved):
+    """The periodic save is collective; it is taken only after the boundary vote passed on
+    every rank. Rank 1 fails in step 3 (the save is due at boundary 4): every rank stops at
+    that vote and takes the error path's save (step 3 when the step was poisoned, 4 when it
+    completed validly) — no rank is left inside the periodic save's collectives."""
+    d = str(tmp_path)
+    write_fake_sbatch(d)
+    args = _base(d, "zero1") + ["--save-every", "4", "--peer-timeout", "20"]
+    procs = _launch(d, "960", args, 2, {"FT_INJECT_FAULT": f"1:3:{phase}"})
+    rcs, waited = _wait_all(procs, timeout=240)
+    logs = _logs(d, "960", 2)
+    assert rcs == [0, 0], logs
+    assert _saved_steps(logs) == [saved, saved], logs
+    assert not any("Checkpoint written" in o for o in logs), logs  # the periodic save never started
+    assert not any("Lost a peer rank" in o for o in logs), logs
+    _assert_same_state(_load(d, "960"), _reference_at(d, "zero1", 2, saved))
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_sigkilled_rank_zero1_resumes_from_periodic_save(tmp_path, world):
+    """ZeRO-1 (the default DP mode) cannot write a checkpoint without the dead rank's optimizer
+    shards; the periodic saves (on by default under DP) are the recovery point. A rank is
+    SIGKILLed after a periodic save became durable: the survivors exit non-zero within the
+    peer timeout naming that checkpoint, and a job resumed from it reaches the same state,
+    bit for bit, as an uninterrupted run."""
+    d = str(tmp_path)
+    write_fake_sbatch(d)
+    args = _base(d, "zero1", steps=10000) + ["--save-every", "4", "--peer-timeout", "20"]
+    procs = _launch(d, "970", args, world, {"FT_INJECT_FAULT": "1:10:kill"})
+    try:
+        assert procs[1].wait(timeout=240) == -signal.SIGKILL
+        t_kill = time.time()
+        rcs = [p.wait(timeout=60) for i, p in enumerate(procs) if i != 1]
+        waited = time.time() - t_kill
+    finally:
+        for p in procs:
+            kill_group(p)
+    logs = _logs(d, "970", world)
+    survivors = [o for i, o in enumerate(logs) if i != 1]
+    assert rcs == [1] * (world - 1), logs
+    assert waited < 30, waited
+    assert all("Lost a peer rank" in o for o in survivors), survivors
+    assert _saved_steps(survivors) == [], survivors  # no new file without the lost shards
+    durable = {int(m.group(1)) for m in (re.search(r"Last durable checkpoint: .* at step (\d+)", o)
+                                         for o in survivors) if m}
+    assert len(durable) == 1 and durable <= {4, 8}, survivors
+    n = durable.pop()
+    assert _load(d, "970")["training_step"] == n
+
+    # resume from the periodic checkpoint to step 14 and compare with an uninterrupted run
+    resume = _base(d, "zero1", steps=16) + ["--checkpoint-id", "970", "--raise-error", "--error-step", "14"]
+    rcs, _ = _wait_all(_launch(d, "971", resume, world))
+    logs = _logs(d, "971", world)
+    assert rcs == [0] * world, logs
+    assert f"Resuming training from training_step {n}" in logs[0], logs[0]
+    assert _saved_steps(logs) == [14] * world, logs
+    _assert_same_state(_load(d, "971"), _reference_at(d, "zero1", world, 14, ["--training-steps", "16"]))
