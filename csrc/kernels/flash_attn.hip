@@ -174,7 +174,7 @@ __device__ __forceinline__ void map_head(int hh, int Hq, int Hkv, int& h, int& k
 template <int D, int NW = 4, int SPLIT = 1>
 __global__ __launch_bounds__(64 * NW * SPLIT, 8 / (NW * SPLIT)) void flash_fwd_kernel(
     const bf16_t* __restrict__ qk, const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out,
-    float* __restrict__ lse2, int B, int S, int Hq, int Hkv, float sl2) {
+    float* __restrict__ lse2, int B, int S, int Hq, int Hkv, float sl2, long ldqk_) {
   constexpr int BM = 32 * NW, BN = 64, KS = D / 16, NDB = D / 32;
   constexpr int TILE = BN * D * 2;
   // K | V tiles by LDS-DMA into two separate LDS objects, loop unrolled by two (as in the
@@ -203,7 +203,7 @@ __global__ __launch_bounds__(64 * NW * SPLIT, 8 / (NW * SPLIT)) void flash_fwd_k
   const int half = (tid >> 6) / NW, wave = (tid >> 6) % NW;  // key-tile parity, query group
   const int q0 = qt * BM + wave * 32;
   const int qrow = q0 + l32;
-  const long ldqk = (long)(Hq + Hkv) * D, ldv = (long)(Hq + 2 * Hkv) * D, ldo = (long)Hq * D;
+  const long ldqk = ldqk_, ldv = (long)(Hq + 2 * Hkv) * D, ldo = (long)Hq * D;
   const bf16_t* Qg = qk + (long)b * S * ldqk + (long)h * D;
   const bf16_t* Kg = qk + (long)b * S * ldqk + (long)(Hq + kvh) * D;
   const bf16_t* Vg = qkv + (long)b * S * ldv + (long)(Hq + Hkv + kvh) * D;
@@ -427,7 +427,7 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_kernel(
     const bf16_t* __restrict__ dO, const bf16_t* __restrict__ qk, const bf16_t* __restrict__ qkv,
     const float* __restrict__ lse2, const float* __restrict__ delta, float* __restrict__ dq_acc,
     bf16_t* __restrict__ dk_part, bf16_t* __restrict__ dv_part, int B, int S, int Hq, int Hkv,
-    float sl2, float scale) {
+    float sl2, float scale, long ldqk_) {
   constexpr int BK = 128, BQ = 32, KS = D / 16, NDB = D / 32, DCH = D / 8;
   constexpr int KIMG = BK * D * 2;   // K image (keys x D)
   constexpr int QIMG = BQ * D * 2;   // one Q or dO slice
@@ -452,7 +452,7 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_kernel(
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, l32 = lane & 31, hi = lane >> 5;
   const int kb0 = kt * BK;
   const int kw = kb0 + wave * 32;  // this wave's first key
-  const long ldqk = (long)(Hq + Hkv) * D, ldv = (long)(Hq + 2 * Hkv) * D, ldo = (long)Hq * D;
+  const long ldqk = ldqk_, ldv = (long)(Hq + 2 * Hkv) * D, ldo = (long)Hq * D;
   const bf16_t* Qg = qk + (long)b * S * ldqk + (long)h * D;
   const bf16_t* Kg = qk + (long)b * S * ldqk + (long)(Hq + kvh) * D;
   const bf16_t* Vg = qkv + (long)b * S * ldv + (long)(Hq + Hkv + kvh) * D;
@@ -668,7 +668,7 @@ template <int D, int NW = 4, int SPLIT = 1>
 __global__ __launch_bounds__(64 * NW * SPLIT, SPLIT == 1 ? 4 / NW : 8 / (NW * SPLIT)) void flash_bwd_dkdv2_kernel(
     const bf16_t* __restrict__ dO, const bf16_t* __restrict__ qk, const bf16_t* __restrict__ qkv,
     const float* __restrict__ lse2, const float* __restrict__ delta, bf16_t* __restrict__ dk_part,
-    bf16_t* __restrict__ dv_part, long ldkv, int B, int S, int Hq, int Hkv, float sl2, float scale) {
+    bf16_t* __restrict__ dv_part, long ldkv, int B, int S, int Hq, int Hkv, float sl2, float scale, long ldqk_) {
   constexpr int BK = 32 * NW, BQ = 32, KS = D / 16, NDB = D / 32;
   constexpr int QIMG = BQ * D * 2;          // one Q or dO slice
   constexpr int SLOT = 2 * QIMG + 256;      // Q | dO | lse[32] | delta[32] of one slice
@@ -687,7 +687,7 @@ __global__ __launch_bounds__(64 * NW * SPLIT, SPLIT == 1 ? 4 / NW : 8 / (NW * SP
   const int hs = (tid >> 6) / NW, wave = (tid >> 6) % NW;  // half-block (pair parity), key group
   const int kb0 = kt * BK;
   const int kw = kb0 + wave * 32;  // this wave's first key
-  const long ldqk = (long)(Hq + Hkv) * D, ldv = (long)(Hq + 2 * Hkv) * D, ldo = (long)Hq * D;
+  const long ldqk = ldqk_, ldv = (long)(Hq + 2 * Hkv) * D, ldo = (long)Hq * D;
   const bf16_t* Qg = qk + (long)b * S * ldqk + (long)h * D;
   const bf16_t* Kg = qk + (long)b * S * ldqk + (long)(Hq + kvh) * D;
   const bf16_t* Vg = qkv + (long)b * S * ldv + (long)(Hq + Hkv + kvh) * D;
@@ -898,7 +898,7 @@ template <int D, int NW = 4, int SPLIT = 1>
 __global__ __launch_bounds__(64 * NW * SPLIT, SPLIT == 1 ? 4 / NW : 8 / (NW * SPLIT)) void flash_bwd_dq_kernel(
     const bf16_t* __restrict__ dO, const bf16_t* __restrict__ qk, const bf16_t* __restrict__ qkv,
     const float* __restrict__ lse2, const float* __restrict__ delta, bf16_t* __restrict__ dqkv, int B,
-    int S, int Hq, int Hkv, float sl2, float scale) {
+    int S, int Hq, int Hkv, float sl2, float scale, long ldqk_) {
   constexpr int BM = 32 * NW, BN = 64, KS = D / 16, NDB = D / 32;
   constexpr int TILE = BN * D * 2;
   // K | V tiles arrive by LDS-DMA (no staging VGPRs held across the compute: at one wave
@@ -923,7 +923,7 @@ __global__ __launch_bounds__(64 * NW * SPLIT, SPLIT == 1 ? 4 / NW : 8 / (NW * SP
   const int half = (tid >> 6) / NW, wave = (tid >> 6) % NW;  // key-tile parity, query group
   const int q0 = qt * BM + wave * 32;
   const int qrow = q0 + l32;
-  const long ldqk = (long)(Hq + Hkv) * D, ldv = (long)(Hq + 2 * Hkv) * D, ldo = (long)Hq * D;
+  const long ldqk = ldqk_, ldv = (long)(Hq + 2 * Hkv) * D, ldo = (long)Hq * D;
   const bf16_t* Qg = qk + (long)b * S * ldqk + (long)h * D;
   const bf16_t* Kg = qk + (long)b * S * ldqk + (long)(Hq + kvh) * D;
   const bf16_t* Vg = qkv + (long)b * S * ldv + (long)(Hq + Hkv + kvh) * D;
@@ -1157,7 +1157,9 @@ void check_inputs(const at::Tensor& qk, const at::Tensor& qkv, int64_t S, int64_
   FT_CHECK_CONTIG(qkv);
   TORCH_CHECK(D == 64 || D == 128, "flash: head_dim must be 64 or 128");
   TORCH_CHECK(Hq % Hkv == 0, "flash: Hq must be a multiple of Hkv");
-  TORCH_CHECK(qk.size(-1) == (Hq + Hkv) * D, "flash: qk width");
+  // qk: the rotated [T, (Hq + Hkv) D] Q/K buffer, or the qkv buffer itself when the QKV projection
+  // rotated Q/K in its epilogue (gemm_qkv_rope_w4); the kernels take its row stride
+  TORCH_CHECK(qk.size(-1) == (Hq + Hkv) * D || qk.size(-1) == (Hq + 2 * Hkv) * D, "flash: qk width");
   TORCH_CHECK(qkv.size(-1) == (Hq + 2 * Hkv) * D, "flash: qkv width");
   TORCH_CHECK(qk.size(0) == qkv.size(0) && qk.size(0) % S == 0, "flash: rows");
 }
@@ -1176,6 +1178,7 @@ std::tuple<at::Tensor, at::Tensor> flash_fwd(const at::Tensor& qk, const at::Ten
   auto out = at::empty({T, Hq * D}, qk.options());
   auto lse = at::empty({B, Hq, (long)stat_stride(S)}, qk.options().dtype(at::kFloat));
   const float sl2 = LOG2E_F / std::sqrt((float)D);
+  const long ldqk = qk.size(-1);
   const int nw = 4;  // see waves_per_block
   const int nqt = (S + 32 * nw - 1) / (32 * nw);
   // key-split blocks when the grid is at most one block per CU (FT_FLASH_FWD_SPLIT=0/1 forces)
@@ -1184,7 +1187,7 @@ std::tuple<at::Tensor, at::Tensor> flash_fwd(const at::Tensor& qk, const at::Ten
 #define FT_FWD(DD, SP)                                                                             \
   hipLaunchKernelGGL((flash_fwd_kernel<DD, 4, SP>), grid, block, 0, ft_stream(), cptr<bf16_t>(qk), \
                      cptr<bf16_t>(qkv), mptr<bf16_t>(out), mptr<float>(lse), B, (int)S, (int)Hq,   \
-                     (int)Hkv, sl2)
+                     (int)Hkv, sl2, ldqk)
   if (D == 128) {
     if (split) FT_FWD(128, 2); else FT_FWD(128, 1);
   } else {
@@ -1228,6 +1231,7 @@ at::Tensor flash_bwd(const at::Tensor& dout, const at::Tensor& qk, const at::Ten
   const long ldkv = direct ? (long)(Hq + 2 * Hkv) * D : (long)Hq * D;
   const float sl2 = LOG2E_F / std::sqrt((float)D);
   const float scale = 1.f / std::sqrt((float)D);
+  const long ldqk = qk.size(-1);
   const long rows = (long)T * Hq;
   const int pre_blocks = (int)((rows * 16 + 255) / 256);
   const int nkt = (S + 127) / 128;
@@ -1240,7 +1244,7 @@ at::Tensor flash_bwd(const at::Tensor& dout, const at::Tensor& qk, const at::Ten
   hipLaunchKernelGGL((flash_bwd_kernel<DD, MODE>), grid, block, 0, ft_stream(), cptr<bf16_t>(dout), \
                      cptr<bf16_t>(qk), cptr<bf16_t>(qkv), cptr<float>(lse), cptr<float>(delta),     \
                      dqp, dkp, dvp, B, (int)S, (int)Hq, (int)Hkv,                                    \
-                     sl2, scale)
+                     sl2, scale, ldqk)
   // dK/dV split, head_dim 64 only (at 128 the doubled block spills): FT_FLASH_KV_SPLIT=0/1
   // forces; default: grids of at most one wave per SIMD
   const bool kv_split = D == 64 && (g_kv_split >= 0 ? g_kv_split == 1 : (long)grid2.x * nw <= 1024);
@@ -1248,7 +1252,7 @@ at::Tensor flash_bwd(const at::Tensor& dout, const at::Tensor& qk, const at::Ten
   hipLaunchKernelGGL((flash_bwd_dkdv2_kernel<DD, NW_, SP_>), grid2, dim3(64 * NW_ * SP_), 0, ft_stream(), \
                      cptr<bf16_t>(dout), cptr<bf16_t>(qk), cptr<bf16_t>(qkv), cptr<float>(lse),           \
                      cptr<float>(delta), dkp, dvp, ldkv, B, (int)S,                                       \
-                     (int)Hq, (int)Hkv, sl2, scale)
+                     (int)Hq, (int)Hkv, sl2, scale, ldqk)
   // dQ key split by default (FT_FLASH_DQ_SPLIT=0 turns it off): S = 2048, 12 heads of 64:
   // 94 -> 83 us for the whole backward; 8B layer 173 -> 167 us; S = 16384 1006 -> 972 us
   // (profiles/r2_flash_key_split.log)
@@ -1257,11 +1261,11 @@ at::Tensor flash_bwd(const at::Tensor& dout, const at::Tensor& qk, const at::Ten
   if (dq_split)                                                                                         \
     hipLaunchKernelGGL((flash_bwd_dq_kernel<DD, NW_, 2>), grid2, dim3(128 * NW_), 0, ft_stream(),       \
                        cptr<bf16_t>(dout), cptr<bf16_t>(qk), cptr<bf16_t>(qkv), cptr<float>(lse),       \
-                       cptr<float>(delta), mptr<bf16_t>(dqkv), B, (int)S, (int)Hq, (int)Hkv, sl2, scale); \
+                       cptr<float>(delta), mptr<bf16_t>(dqkv), B, (int)S, (int)Hq, (int)Hkv, sl2, scale, ldqk); \
   else                                                                                                  \
     hipLaunchKernelGGL((flash_bwd_dq_kernel<DD, NW_, 1>), grid2, block2, 0, ft_stream(),                \
                        cptr<bf16_t>(dout), cptr<bf16_t>(qk), cptr<bf16_t>(qkv), cptr<float>(lse),       \
-                       cptr<float>(delta), mptr<bf16_t>(dqkv), B, (int)S, (int)Hq, (int)Hkv, sl2, scale)
+                       cptr<float>(delta), mptr<bf16_t>(dqkv), B, (int)S, (int)Hq, (int)Hkv, sl2, scale, ldqk)
   if (D == 128) {
     hipLaunchKernelGGL(flash_bwd_pre_kernel<128>, dim3(pre_blocks), block, 0, ft_stream(),
                        cptr<bf16_t>(dout), cptr<bf16_t>(out), mptr<float>(delta), B, (int)S, (int)Hq);

@@ -145,9 +145,8 @@ class TransformerBlock(nn.Module):
         else:
             h, xn = Fx.add_norm(h, d, self.attention_norm.weight, sk(self.attention_norm.weight), self.eps,
                                 self.layernorm)
-        qkv = Fx.linear(xn, at.wqkv, at.wqkv_sink)
-        o = Fx.rope_attention(qkv.view(-1, qkv.shape[-1]), cos, sin, seq_len, at.n_heads, at.n_kv_heads, at.head_dim,
-                              self.attn_keep if gen is not None else None, -1 if gen is None else gen)
+        o = Fx.qkv_rope_attention(xn, at.wqkv, at.wqkv_sink, cos, sin, seq_len, at.n_heads, at.n_kv_heads,
+                                  at.head_dim, self.attn_keep if gen is not None else None, -1 if gen is None else gen)
         da = Fx.linear(o.view(*h.shape[:-1], -1), at.wo.weight, sk(at.wo.weight))
         h, hn = Fx.add_norm(h, da, self.ffn_norm.weight, sk(self.ffn_norm.weight), self.eps, self.layernorm)
         return h, Fx.feed_forward(hn, ff.w13, ff.w2.weight, ff.w13_sink, sk(ff.w2.weight))

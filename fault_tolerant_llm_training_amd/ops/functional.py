@@ -83,10 +83,31 @@ def _hand(kind: str, M: int, N: int, K: int, *ts) -> bool:
     return kind == "dx" and (M // 256) * (N // 256) < 64 and K >= 16384
 
 
+# Forward GEMMs on the 4-wave hand kernel (csrc/kernels/gemm_w4.hip): FT_W4_FWD=1 routes every
+# fitting x W^T product (T % 256, K % 64, N a multiple of 128/192/224/256) to it.
+_W4_FWD = os.environ.get("FT_W4_FWD", "0") == "1"
+
+
+def set_w4_fwd(on: bool) -> None:
+    global _W4_FWD
+    _W4_FWD = bool(on)
+
+
+def _w4_ok(x2: torch.Tensor, w: torch.Tensor) -> bool:
+    if not (_W4_FWD and _GEMM_MODE != "blas" and x2.is_cuda and x2.dtype == torch.bfloat16
+            and w.dtype == torch.bfloat16):
+        return False
+    T, K = x2.shape
+    return T % 256 == 0 and K % 64 == 0 and kernels().gemm_w4_pick(T, w.shape[0]) > 0
+
+
 def mm_fwd(x2: torch.Tensor, w: torch.Tensor, residual: Optional[torch.Tensor] = None) -> torch.Tensor:
     """y = x2 @ w^T (+ residual): x2 [T, K], w [N, K] (nn.Linear layout)."""
     T, K = x2.shape
     N = w.shape[0]
+    if _w4_ok(x2, w):
+        return kernels().gemm_nt_w4(x2.contiguous(), w, None,
+                                    None if residual is None else residual.reshape(T, N).contiguous(), 0)
     if _hand("fwd", T, N, K, x2, w):
         return kernels().gemm(x2.contiguous(), True, w, True, T, N, K, None,
                               None if residual is None else residual.reshape(T, N).contiguous(), False, 0)
@@ -483,15 +504,21 @@ class AttentionKeep:
 
 
 class RopeAttentionFn(torch.autograd.Function):
+    """RoPE + causal GQA attention on the packed projection. ``rotated``: Q/K of ``qkv`` were
+    already rotated by the QKV projection's epilogue (:class:`QKVRopeFn`, GPU only): the flash
+    kernels then read Q/K straight from ``qkv`` and the gradient is returned in the rotated frame
+    (the projection's backward rotates it back)."""
+
     @staticmethod
-    def forward(ctx, qkv, cos, sin, seq_len, hq, hkv, d, keep=None, gen=-1):
+    def forward(ctx, qkv, cos, sin, seq_len, hq, hkv, d, keep=None, gen=-1, rotated=False):
         ctx.cfg = (seq_len, hq, hkv, d)
+        ctx.rotated = rotated
         hit = keep is not None and keep.gen == gen and keep.o is not None
         if qkv.is_cuda:
             from .attention import flash_attn_fwd
 
             qkv = qkv.contiguous()
-            qk = kernels().rope_fwd(qkv, cos, sin, seq_len, hq, hkv, d)
+            qk = qkv if rotated else kernels().rope_fwd(qkv, cos, sin, seq_len, hq, hkv, d)
             if hit:  # recompute pass of a checkpointed block: the kept output (bit-identical)
                 o, lse = keep.o, keep.lse
                 keep.o = keep.lse = None
@@ -519,20 +546,75 @@ class RopeAttentionFn(torch.autograd.Function):
 
             qkv, qk, o, lse, cos, sin = ctx.saved_tensors
             dqkv = flash_attn_bwd(do.contiguous(), qk, qkv, o, lse, seq_len, hq, hkv, d)
-            kernels().rope_bwd_(dqkv, cos, sin, seq_len, hq, hkv, d)
-            return dqkv, None, None, None, None, None, None, None, None
+            if not ctx.rotated:
+                kernels().rope_bwd_(dqkv, cos, sin, seq_len, hq, hkv, d)
+            return dqkv, None, None, None, None, None, None, None, None, None
         qkv, cos, sin = ctx.saved_tensors
         with torch.enable_grad():
             x = qkv.detach().requires_grad_(True)
             o = attention_reference(x, cos, sin, seq_len, hq, hkv, d)
             (dx,) = torch.autograd.grad(o, (x,), do)
-        return dx, None, None, None, None, None, None, None, None
+        return dx, None, None, None, None, None, None, None, None, None
 
 
-def rope_attention(qkv, cos, sin, seq_len, hq, hkv, d, keep: Optional[AttentionKeep] = None, gen: int = -1):
+def rope_attention(qkv, cos, sin, seq_len, hq, hkv, d, keep: Optional[AttentionKeep] = None, gen: int = -1,
+                   rotated: bool = False):
     """RoPE on the packed projection, then causal GQA attention. ``keep``/``gen``: selective
     activation checkpointing (see :class:`AttentionKeep`)."""
-    return RopeAttentionFn.apply(qkv, cos, sin, seq_len, hq, hkv, d, keep, gen)
+    return RopeAttentionFn.apply(qkv, cos, sin, seq_len, hq, hkv, d, keep, gen, rotated)
+
+
+# QKV projection with RoPE in the GEMM epilogue (csrc/kernels/gemm_w4.hip, gemm_qkv_rope_w4): the
+# hand-written 4-wave GEMM writes qkv with Q/K already rotated, so neither the separate RoPE
+# kernel nor the rotated [T, (Hq + Hkv) D] copy exists; the flash kernels read Q/K from qkv.
+# FT_QKV_ROPE=0 restores hipBLASLt + the RoPE kernel.
+_QKV_ROPE = os.environ.get("FT_QKV_ROPE", "0") == "1"
+
+
+def set_qkv_rope(on: bool) -> None:
+    global _QKV_ROPE
+    _QKV_ROPE = bool(on)
+
+
+def _qkv_rope_ok(x2: torch.Tensor, w: torch.Tensor, d: int) -> bool:
+    if not (_QKV_ROPE and _GEMM_MODE != "blas" and x2.is_cuda and x2.dtype == torch.bfloat16
+            and w.dtype == torch.bfloat16):
+        return False
+    T, K = x2.shape
+    return T % 256 == 0 and K % 64 == 0 and d % 8 == 0 and kernels().gemm_w4_pick(T, w.shape[0]) > 0
+
+
+class QKVRopeFn(torch.autograd.Function):
+    """qkv = x W^T with Q/K rotated (reference model.py:195 then :100-126). Backward receives the
+    gradient in the rotated frame, rotates it back in place (rope_bwd_), then dW / dX."""
+
+    @staticmethod
+    def forward(ctx, x2, w, sink, cos, sin, seq_len, hq, hkv, d):
+        ctx.sink = sink
+        ctx.cfg = (seq_len, hq, hkv, d)
+        ctx.save_for_backward(x2, w, cos, sin)
+        return kernels().gemm_qkv_rope_w4(x2, w, cos, sin, seq_len, hq, hkv, d)
+
+    @staticmethod
+    def backward(ctx, dq):
+        x2, w, cos, sin = ctx.saved_tensors
+        seq_len, hq, hkv, d = ctx.cfg
+        dq = dq.contiguous()
+        kernels().rope_bwd_(dq, cos, sin, seq_len, hq, hkv, d)
+        dw = weight_grad_async(dq, x2, ctx.sink)
+        dx = mm_dx(dq, w)
+        return dx, dw, None, None, None, None, None, None, None
+
+
+def qkv_rope_attention(xn, wqkv, sink, cos, sin, seq_len, hq, hkv, d, keep: Optional[AttentionKeep] = None,
+                       gen: int = -1):
+    """QKV projection + RoPE + causal GQA attention (reference model.py:179-212). Returns o [.., Hq D]."""
+    x2 = xn.reshape(-1, xn.shape[-1])
+    if _qkv_rope_ok(x2, wqkv, d):
+        qkv = QKVRopeFn.apply(x2.contiguous(), wqkv, sink, cos, sin, seq_len, hq, hkv, d)
+        return rope_attention(qkv, cos, sin, seq_len, hq, hkv, d, keep, gen, rotated=True)
+    qkv = linear(xn, wqkv, sink)
+    return rope_attention(qkv.view(-1, qkv.shape[-1]), cos, sin, seq_len, hq, hkv, d, keep, gen)
 
 
 # --------------------------------------------------------------------------------------
@@ -591,14 +673,14 @@ class FeedForwardFn(torch.autograd.Function):
         K_ = kernels()
         D = x.shape[-1]
         x2 = x.reshape(-1, D)
-        gu = torch.mm(x2, w13.t())
+        gu = mm_fwd(x2, w13)
         tn = _use_tn(gu, x2)
         t_only = tn and _FFN_T_ONLY
         if tn:
             a, aT = K_.swiglu_fwd_t(gu, not t_only)
         else:
             a, aT = K_.swiglu_fwd(gu), None
-        y = torch.mm(aT.t() if t_only else a, w2.t())
+        y = torch.mm(aT.t(), w2.t()) if t_only else mm_fwd(a, w2)
         ctx.sinks = (sink13, sink2)
         ctx.tn = tn
         ctx.t_only = t_only

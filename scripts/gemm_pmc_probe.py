@@ -14,7 +14,14 @@ from fault_tolerant_llm_training_amd._native import kernels  # noqa: E402
 M, N, K = (int(v) for v in sys.argv[1:4]) if len(sys.argv) >= 4 else (2048, 28672, 4096)
 layout = sys.argv[4] if len(sys.argv) >= 5 else "fwd"
 k = kernels()
-if layout == "dw":
+if layout == "w4":  # the 4-wave kernel (csrc/kernels/gemm_w4.hip) vs hipBLASLt, forward layout
+    var = int(os.environ.get("FT_W4_VARIANT", "3"))
+    a = (torch.rand(M, K, device="cuda") * 2 - 1).bfloat16()
+    b = (torch.rand(N, K, device="cuda") * 2 - 1).bfloat16()
+    for _ in range(20):
+        k.gemm_nt_w4(a, b, None, None, var)
+        torch.mm(a, b.t())
+elif layout == "dw":
     a = (torch.rand(K, M, device="cuda") * 2 - 1).bfloat16()
     b = (torch.rand(K, N, device="cuda") * 2 - 1).bfloat16()
     for _ in range(20):

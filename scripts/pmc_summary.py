@@ -1,0 +1,11 @@
+import csv, glob, sys, collections
+d = sys.argv[1]
+agg = collections.defaultdict(lambda: collections.defaultdict(list))
+for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
+    for row in csv.DictReader(open(f)):
+        k = row["Kernel_Name"][:60]
+        agg[k][row["Counter_Name"]].append(float(row["Counter_Value"]))
+for k, cs in agg.items():
+    print(k)
+    for c, v in sorted(cs.items()):
+        print(f"   {c:28s} {sum(v)/len(v):16.0f}  (n={len(v)})")

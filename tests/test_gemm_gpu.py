@@ -95,3 +95,51 @@ def test_gemm_swiglu_forward_and_backward():
     du_ref = da * g * s
     ref = torch.cat([dg_ref, du_ref], dim=-1)
     check(dgu, ref, D)
+
+
+@pytest.mark.parametrize("nj", [8, 7, 6, 4])
+@pytest.mark.parametrize("M,K", [(256, 64), (512, 128), (2048, 4096), (768, 640)])
+def test_gemm_w4_tiles(nj, M, K):
+    """4-wave schedule-level GEMM (csrc/kernels/gemm_w4.hip), every tile width, vs fp32; residual."""
+    from fault_tolerant_llm_training_amd._native import kernels
+
+    K_ = kernels()
+    N = 32 * nj * 3
+    torch.manual_seed(M + K + nj)
+    a = (torch.rand(M, K, device="cuda") * 2 - 1).bfloat16()
+    b = (torch.rand(N, K, device="cuda") * 2 - 1).bfloat16()
+    ref = a.float() @ b.float().t()
+    out = K_.gemm_nt_w4(a, b, None, None, nj)
+    assert ((out.float() - ref).norm() / ref.norm()).item() < 4e-3
+    r = (torch.rand(M, N, device="cuda") * 2 - 1).bfloat16()
+    out = K_.gemm_nt_w4(a, b, None, r, nj)
+    ref = ref + r.float()
+    assert ((out.float() - ref).norm() / ref.norm()).item() < 4e-3
+    o2 = torch.empty_like(out)
+    K_.gemm_nt_w4(a, b, o2, r, nj)
+    assert torch.equal(o2, out)  # deterministic
+
+
+@pytest.mark.parametrize("hq,hkv,d,S,B", [(32, 8, 128, 2048, 1), (12, 12, 64, 512, 2), (16, 4, 64, 256, 4)])
+def test_gemm_qkv_rope_w4(hq, hkv, d, S, B):
+    """QKV projection with RoPE in the epilogue == projection (fp32) then the reference RoPE."""
+    from fault_tolerant_llm_training_amd._native import kernels
+    from fault_tolerant_llm_training_amd.models.llama import rope_tables
+    from fault_tolerant_llm_training_amd.ops.functional import rope_reference
+
+    K_ = kernels()
+    D = 1024 if hq * d <= 1024 else 4096
+    W = (hq + 2 * hkv) * d
+    torch.manual_seed(hq)
+    x = (torch.rand(B * S, D, device="cuda") * 2 - 1).bfloat16()
+    w = ((torch.rand(W, D, device="cuda") * 2 - 1) / D ** 0.5).bfloat16()
+    cos, sin = rope_tables(d, S, 500000.0)
+    cos, sin = cos.cuda(), sin.cuda()
+    if K_.gemm_w4_pick(B * S, W) == 0:
+        pytest.skip("no w4 tile width for this N")
+    out = K_.gemm_qkv_rope_w4(x, w, cos, sin, S, hq, hkv, d)
+    y = (x.float() @ w.float().t()).bfloat16()  # the unfused path rotates the bf16 projection
+    q = rope_reference(y[:, : hq * d].view(B, S, hq, d), cos, sin).reshape(B * S, -1)
+    k = rope_reference(y[:, hq * d : (hq + hkv) * d].view(B, S, hkv, d), cos, sin).reshape(B * S, -1)
+    ref = torch.cat([q, k, y[:, (hq + hkv) * d :]], 1).float()
+    assert ((out.float() - ref).norm() / ref.norm()).item() < 6e-3
