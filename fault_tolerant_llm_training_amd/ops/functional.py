@@ -83,9 +83,14 @@ def _hand(kind: str, M: int, N: int, K: int, *ts) -> bool:
     return kind == "dx" and (M // 256) * (N // 256) < 64 and K >= 16384
 
 
-# Forward GEMMs on the 4-wave hand kernel (csrc/kernels/gemm_w4.hip): FT_W4_FWD=1 routes every
-# fitting x W^T product (T % 256, K % 64, N a multiple of 128/192/224/256) to it.
-_W4_FWD = os.environ.get("FT_W4_FWD", "0") == "1"
+# GEMMs on the 4-wave hand kernel (csrc/kernels/gemm_w4.hip), K-contiguous operands (x W^T):
+#   FT_W4_FWD    (default on) forward products whose tile width is narrower than 256 (it fills the
+#                256 CUs in whole rounds where the 256-wide vendor tiles leave a partial round:
+#                Llama-3-8B qkv 1.14x, wo 1.09x, w2 1.02x of hipBLASLt; w13 / LM head stay on it)
+#   FT_W4_DW=1   weight gradients dW = dY^T X on the transposed operands (every size)
+_W4_FWD = os.environ.get("FT_W4_FWD", "1") != "0"
+_W4_DW = os.environ.get("FT_W4_DW", "0") == "1"
+_W4_FWD_MAX_NJ = int(os.environ.get("FT_W4_FWD_MAX_NJ", "6"))
 
 
 def set_w4_fwd(on: bool) -> None:
@@ -93,12 +98,25 @@ def set_w4_fwd(on: bool) -> None:
     _W4_FWD = bool(on)
 
 
-def _w4_ok(x2: torch.Tensor, w: torch.Tensor) -> bool:
-    if not (_W4_FWD and _GEMM_MODE != "blas" and x2.is_cuda and x2.dtype == torch.bfloat16
-            and w.dtype == torch.bfloat16):
+def set_w4_dw(on: bool) -> None:
+    global _W4_DW
+    _W4_DW = bool(on)
+
+
+def _w4_fits(x2: torch.Tensor, w: torch.Tensor, max_nj: int = 8) -> bool:
+    if _GEMM_MODE == "blas" or not (x2.is_cuda and x2.dtype == torch.bfloat16 and w.dtype == torch.bfloat16):
         return False
     T, K = x2.shape
-    return T % 256 == 0 and K % 64 == 0 and kernels().gemm_w4_pick(T, w.shape[0]) > 0
+    if T % 256 or K % 64:
+        return False
+    nj = kernels().gemm_w4_pick(T, w.shape[0])
+    # at least half the chip in tiles: smaller products (GPT-2-sized, K = 768-1024) are
+    # latency-bound and stay on the vendor kernels
+    return 0 < nj <= max_nj and (T // 256) * (w.shape[0] // (32 * nj)) >= 128
+
+
+def _w4_ok(x2: torch.Tensor, w: torch.Tensor) -> bool:
+    return _W4_FWD and _w4_fits(x2, w, _W4_FWD_MAX_NJ)
 
 
 def mm_fwd(x2: torch.Tensor, w: torch.Tensor, residual: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -141,6 +159,8 @@ def _use_tn(dy2: torch.Tensor, x2: torch.Tensor) -> bool:
     K = x2.shape[1]
     if T % 64 or N % 64 or K % 64:
         return False
+    if _W4_DW and T % 64 == 0 and N % 256 == 0 and kernels().gemm_w4_pick(N, K) > 0:
+        return True  # the w4 kernel runs dW on the transposed (K-contiguous) operands
     return _DW_MODE == "all" or 2.0 * T * N * K >= _DW_MIN_FLOP
 
 
@@ -180,6 +200,13 @@ def weight_grad(dy2: torch.Tensor, x2: torch.Tensor, sink: Optional[GradSink],
         ba, bb = bufs if bufs is not None else (None, None)
         a = dyT if dyT is not None else K_.transpose2d(dy2.contiguous(), ba)   # [N, T]
         b = xT if xT is not None else K_.transpose2d(x2.contiguous(), bb)      # [K, T]
+        if _W4_DW and _w4_fits(a, b):
+            if sink is not None:
+                out = sink.buf.view(N, K)
+                K_.gemm_nt_w4(a, b, out, out if sink.accumulate else None, 0)
+                sink.ready()
+                return None
+            return K_.gemm_nt_w4(a, b, None, None, 0)
         if sink is not None:
             sink.mm(a, b.t())
             return None
@@ -567,8 +594,10 @@ def rope_attention(qkv, cos, sin, seq_len, hq, hkv, d, keep: Optional[AttentionK
 # QKV projection with RoPE in the GEMM epilogue (csrc/kernels/gemm_w4.hip, gemm_qkv_rope_w4): the
 # hand-written 4-wave GEMM writes qkv with Q/K already rotated, so neither the separate RoPE
 # kernel nor the rotated [T, (Hq + Hkv) D] copy exists; the flash kernels read Q/K from qkv.
+# Default on (8B step: 1.001-1.003x, the RoPE forward kernel and the rotated copy gone; the
+# kernel alone runs the Llama-3-8B QKV shape at 1.10-1.14x hipBLASLt, profiles/r3_gemm_w4_investigation.md);
 # FT_QKV_ROPE=0 restores hipBLASLt + the RoPE kernel.
-_QKV_ROPE = os.environ.get("FT_QKV_ROPE", "0") == "1"
+_QKV_ROPE = os.environ.get("FT_QKV_ROPE", "1") != "0"
 
 
 def set_qkv_rope(on: bool) -> None:
@@ -580,8 +609,7 @@ def _qkv_rope_ok(x2: torch.Tensor, w: torch.Tensor, d: int) -> bool:
     if not (_QKV_ROPE and _GEMM_MODE != "blas" and x2.is_cuda and x2.dtype == torch.bfloat16
             and w.dtype == torch.bfloat16):
         return False
-    T, K = x2.shape
-    return T % 256 == 0 and K % 64 == 0 and d % 8 == 0 and kernels().gemm_w4_pick(T, w.shape[0]) > 0
+    return d % 8 == 0 and _w4_fits(x2, w)
 
 
 class QKVRopeFn(torch.autograd.Function):

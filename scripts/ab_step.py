@@ -13,7 +13,8 @@ Knobs toggled between timing windows (alternating rounds, so box and clock drift
   tonly — SwiGLU kernels write only the transposed activation/gradient; the w2 forward and
           w13 dX GEMMs read them as A^T
   qkvrope — QKV projection on the 4-wave hand GEMM with RoPE in its epilogue (no RoPE kernel)
-  w4fwd — every forward x W^T GEMM on the 4-wave hand GEMM (csrc/kernels/gemm_w4.hip)
+  w4fwd — forward x W^T GEMMs with narrow tiles on the 4-wave hand GEMM (csrc/kernels/gemm_w4.hip)
+  w4dw  — weight gradients on the 4-wave hand GEMM (transposed operands)
 Usage: python scripts/ab_step.py [--steps 8] [--rounds 3] [--configs gemm,dw ...]
 """
 from __future__ import annotations
@@ -112,7 +113,7 @@ def main():
                "hand_dw_wo_w2": shapes("dw:4096x4096x2048,dw:4096x14336x2048"),
                "hand_dw_wo": shapes("dw:4096x4096x2048"), "dw": Fx.set_dw_stream, "tonly": Fx.set_ffn_t_only,
                "dkdv2": kernels().flash_set_dkdv2, "prio": set_prio, "sumsq_end": ddp_mod.set_sumsq_at_end,
-               "qkvrope": Fx.set_qkv_rope, "w4fwd": Fx.set_w4_fwd}
+               "qkvrope": Fx.set_qkv_rope, "w4fwd": Fx.set_w4_fwd, "w4dw": Fx.set_w4_dw}
     configs = list(itertools.product([False, True], repeat=len(knobs)))
 
     def apply(cfg):

@@ -43,7 +43,9 @@ for M, N, K in [(256, 256, 64), (2048, 6144, 4096), (768, 1792, 640)]:
             sys.exit(1)
 rounds = int(sys.argv[sys.argv.index("--rounds") + 1]) if "--rounds" in sys.argv else 3
 T, D, F, V = 2048, 4096, 14336, 131072
-shapes = [("qkv", T, 6144, D), ("wo", T, D, D), ("w13", T, 2 * F, D), ("w2", T, D, F), ("head", T, V, D)]
+shapes = [("qkv", T, 6144, D), ("wo", T, D, D), ("w13", T, 2 * F, D), ("w2", T, D, F), ("head", T, V, D),
+          # weight gradients dW[N_out, K_in] = dY^T X on the transposed operands (NT, K = tokens)
+          ("dWqkv", 6144, D, T), ("dWwo", D, D, T), ("dWw13", 2 * F, D, T), ("dWw2", D, F, T), ("dWhead", V, D, T)]
 res = {}
 for rd in range(rounds):
     for name, M, N, K in shapes:

@@ -143,3 +143,28 @@ def test_gemm_qkv_rope_w4(hq, hkv, d, S, B):
     k = rope_reference(y[:, hq * d : (hq + hkv) * d].view(B, S, hkv, d), cos, sin).reshape(B * S, -1)
     ref = torch.cat([q, k, y[:, (hq + hkv) * d :]], 1).float()
     assert ((out.float() - ref).norm() / ref.norm()).item() < 6e-3
+
+
+@pytest.mark.parametrize("T,N,Kd", [(2048, 6144, 4096), (512, 1024, 768)])
+def test_weight_grad_on_w4(T, N, Kd):
+    """dW = dY^T X through the 4-wave kernel (transposed operands) into a gradient sink, written
+    and accumulated (gradient accumulation), vs fp32."""
+    from fault_tolerant_llm_training_amd.ops import functional as Fx
+    from fault_tolerant_llm_training_amd.ops.grad_sink import GradSink
+
+    torch.manual_seed(T + N)
+    dy = rnd(T, N)
+    x = rnd(T, Kd)
+    buf = torch.zeros(N * Kd, device="cuda", dtype=torch.bfloat16)
+    sink = GradSink(buf, 0, N * Kd)
+    old = Fx._W4_DW
+    Fx.set_w4_dw(True)
+    try:
+        Fx.weight_grad(dy, x, sink)
+        ref = dy.float().t() @ x.float()
+        assert ((buf.view(N, Kd).float() - ref).norm() / ref.norm()).item() < 4e-3
+        sink.accumulate = True
+        Fx.weight_grad(dy, x, sink)
+        assert ((buf.view(N, Kd).float() - 2 * ref).norm() / (2 * ref).norm()).item() < 6e-3
+    finally:
+        Fx.set_w4_dw(old)
