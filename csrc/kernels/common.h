@@ -9,6 +9,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #define FT_WAVE 64
 
 typedef uint16_t bf16_t;
@@ -47,6 +49,75 @@ __device__ __forceinline__ uint4 pack8(const float* f) {
   r.z = pack2(f[4], f[5]);
   r.w = pack2(f[6], f[7]);
   return r;
+}
+
+// ---- element types of the model dtype (--model-dtype bf16 / fp16 / fp32, reference utils.py:14-19):
+// storage T, math in fp32. 8 elements move per access: 16 B for the 16-bit types, 32 B for fp32.
+struct EBF16 {
+  typedef uint16_t T;
+  static constexpr bool is16 = true;
+};
+struct EF16 {
+  typedef uint16_t T;
+  static constexpr bool is16 = true;
+};
+struct EF32 {
+  typedef float T;
+  static constexpr bool is16 = false;
+};
+
+__device__ __forceinline__ float h2f(uint16_t v) { return (float)__builtin_bit_cast(_Float16, v); }
+__device__ __forceinline__ uint16_t f2h(float f) { return __builtin_bit_cast(uint16_t, (_Float16)f); }
+
+template <class E>
+__device__ __forceinline__ float ld1(const typename E::T* p) {
+  if constexpr (std::is_same<E, EBF16>::value) return bf2f(*p);
+  else if constexpr (std::is_same<E, EF16>::value) return h2f(*p);
+  else return *p;
+}
+
+template <class E>
+__device__ __forceinline__ typename E::T cvt1(float f) {
+  if constexpr (std::is_same<E, EBF16>::value) return f2bf(f);
+  else if constexpr (std::is_same<E, EF16>::value) return f2h(f);
+  else return f;
+}
+
+template <class E>
+__device__ __forceinline__ void ld8(const typename E::T* p, float* f) {
+  if constexpr (std::is_same<E, EBF16>::value) {
+    unpack8(*reinterpret_cast<const uint4*>(p), f);
+  } else if constexpr (std::is_same<E, EF16>::value) {
+    const uint4 v = *reinterpret_cast<const uint4*>(p);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      f[2 * i] = h2f((uint16_t)(w[i] & 0xffffu));
+      f[2 * i + 1] = h2f((uint16_t)(w[i] >> 16));
+    }
+  } else {
+    const float4 a = *reinterpret_cast<const float4*>(p);
+    const float4 b = *reinterpret_cast<const float4*>(p + 4);
+    f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w;
+    f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
+  }
+}
+
+template <class E>
+__device__ __forceinline__ void st8(typename E::T* p, const float* f) {
+  if constexpr (std::is_same<E, EBF16>::value) {
+    *reinterpret_cast<uint4*>(p) = pack8(f);
+  } else if constexpr (std::is_same<E, EF16>::value) {
+    uint4 v;
+    v.x = (uint32_t)f2h(f[0]) | ((uint32_t)f2h(f[1]) << 16);
+    v.y = (uint32_t)f2h(f[2]) | ((uint32_t)f2h(f[3]) << 16);
+    v.z = (uint32_t)f2h(f[4]) | ((uint32_t)f2h(f[5]) << 16);
+    v.w = (uint32_t)f2h(f[6]) | ((uint32_t)f2h(f[7]) << 16);
+    *reinterpret_cast<uint4*>(p) = v;
+  } else {
+    *reinterpret_cast<float4*>(p) = make_float4(f[0], f[1], f[2], f[3]);
+    *reinterpret_cast<float4*>(p + 4) = make_float4(f[4], f[5], f[6], f[7]);
+  }
 }
 
 __device__ __forceinline__ float wave_sum(float v) {

@@ -20,14 +20,15 @@
 
 namespace {
 
+// row copy in 16-B vectors (any element size; rows are whole vectors)
 __global__ __launch_bounds__(256) void emb_fwd_kernel(const int64_t* __restrict__ tok,
-                                                      const bf16_t* __restrict__ w,
-                                                      bf16_t* __restrict__ out, int T, int D) {
+                                                      const char* __restrict__ w,
+                                                      char* __restrict__ out, int T, int row_bytes) {
   const int row = blockIdx.x;
   const int64_t t = tok[row];
-  const uint4* src = reinterpret_cast<const uint4*>(w + t * (long)D);
-  uint4* dst = reinterpret_cast<uint4*>(out + (long)row * D);
-  for (int c = threadIdx.x; c < D / 8; c += blockDim.x) dst[c] = src[c];
+  const uint4* src = reinterpret_cast<const uint4*>(w + t * (long)row_bytes);
+  uint4* dst = reinterpret_cast<uint4*>(out + (long)row * row_bytes);
+  for (int c = threadIdx.x; c < row_bytes / 16; c += blockDim.x) dst[c] = src[c];
 }
 
 constexpr int SORT_NT = 1024, SORT_W = SORT_NT / 64, SORT_BITS = 6, SORT_BINS = 1 << SORT_BITS;
@@ -101,10 +102,11 @@ __global__ __launch_bounds__(SORT_NT) void tok_sort_kernel(const int64_t* __rest
 }
 
 // sorted_tok[i], perm[i]: i-th smallest token and its original row.
+template <class E>
 __global__ __launch_bounds__(256) void emb_bwd_kernel(const int* __restrict__ sorted_tok,
                                                       const int* __restrict__ perm,
-                                                      const bf16_t* __restrict__ dy,
-                                                      bf16_t* __restrict__ dw, int T, int D,
+                                                      const typename E::T* __restrict__ dy,
+                                                      typename E::T* __restrict__ dw, int T, int D,
                                                       bool accumulate) {
   const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
@@ -113,22 +115,22 @@ __global__ __launch_bounds__(256) void emb_bwd_kernel(const int* __restrict__ so
   if (wave > 0 && sorted_tok[wave - 1] == t) return;  // not the segment head
   int end = wave + 1;
   while (end < T && sorted_tok[end] == t) ++end;
-  bf16_t* dst = dw + t * (long)D;
+  typename E::T* dst = dw + t * (long)D;
   for (int c = lane * 8; c < D; c += 64 * 8) {
     float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (int k = wave; k < end; ++k) {
       float x[8];
-      unpack8(*reinterpret_cast<const uint4*>(dy + perm[k] * (long)D + c), x);
+      ld8<E>(dy + perm[k] * (long)D + c, x);
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[j] += x[j];
     }
     if (accumulate) {
       float o[8];
-      unpack8(*reinterpret_cast<const uint4*>(dst + c), o);
+      ld8<E>(dst + c, o);
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[j] += o[j];
     }
-    *reinterpret_cast<uint4*>(dst + c) = pack8(acc);
+    st8<E>(dst + c, acc);
   }
 }
 
@@ -136,7 +138,7 @@ __global__ __launch_bounds__(256) void emb_bwd_kernel(const int* __restrict__ so
 
 at::Tensor embedding_fwd(const at::Tensor& tokens, const at::Tensor& weight) {
   FT_CHECK_CUDA(weight);
-  FT_CHECK_BF16(weight);
+  FT_CHECK_MODEL_DTYPE(weight);
   FT_CHECK_CONTIG(weight);
   FT_CHECK_CONTIG(tokens);
   TORCH_CHECK(tokens.scalar_type() == at::kLong, "embedding: tokens must be int64");
@@ -149,7 +151,7 @@ at::Tensor embedding_fwd(const at::Tensor& tokens, const at::Tensor& weight) {
   auto out = at::empty(sizes, weight.options());
   if (T > 0)
     hipLaunchKernelGGL(emb_fwd_kernel, dim3(T), dim3(256), 0, ft_stream(), cptr<int64_t>(tokens),
-                       cptr<bf16_t>(weight), mptr<bf16_t>(out), T, D);
+                       cptr<char>(weight), mptr<char>(out), T, (int)(D * weight.element_size()));
   FT_LAUNCH_CHECK();
   return out;
 }
@@ -158,7 +160,8 @@ at::Tensor embedding_fwd(const at::Tensor& tokens, const at::Tensor& weight) {
 void embedding_bwd_(const at::Tensor& dy, const at::Tensor& tokens, const at::Tensor& dw,
                     bool accumulate) {
   FT_CHECK_CUDA(dy);
-  FT_CHECK_BF16(dy);
+  FT_CHECK_MODEL_DTYPE(dy);
+  TORCH_CHECK(dy.scalar_type() == dw.scalar_type(), "embedding_bwd: dtype mismatch");
   FT_CHECK_CONTIG(dy);
   FT_CHECK_CONTIG(dw);
   const int D = dw.size(1);
@@ -182,8 +185,9 @@ void embedding_bwd_(const at::Tensor& dy, const at::Tensor& tokens, const at::Te
     FT_LAUNCH_CHECK();
     const long fin = (long)((passes - 1) & 1) * T;
     const int blocks = (T * 64 + 255) / 256;
-    hipLaunchKernelGGL(emb_bwd_kernel, dim3(blocks), dim3(256), 0, ft_stream(), keys + fin, vals + fin,
-                       cptr<bf16_t>(dy), mptr<bf16_t>(dw), T, D, accumulate);
+    FT_DISPATCH_E(dy.scalar_type(),
+                  hipLaunchKernelGGL(emb_bwd_kernel<E>, dim3(blocks), dim3(256), 0, ft_stream(), keys + fin,
+                                     vals + fin, cptr<typename E::T>(dy), mptr<typename E::T>(dw), T, D, accumulate));
   }
   FT_LAUNCH_CHECK();
 }

@@ -10,15 +10,15 @@
 // Q and K heads into a packed [T, (Hq+Hkv)*D] buffer that the flash-attention
 // kernel reads directly (V is consumed from the QKV buffer in place, so the
 // reference's repeat_kv copy (model.py:129-138) never exists). Backward rotates
-// dQ/dK in place inside the fused dQKV gradient buffer. Each lane moves 8 bf16
-// (4 pairs) with 16-B accesses.
+// dQ/dK in place inside the fused dQKV gradient buffer. Each lane moves 8 elements
+// (4 pairs): 16-B accesses for bf16 / fp16, 32 B for fp32 (--model-dtype).
 #include "torch_utils.h"
 
 namespace {
 
-template <bool BWD>
-__global__ __launch_bounds__(256) void rope_kernel(const bf16_t* __restrict__ src, int src_stride,
-                                                   bf16_t* __restrict__ dst, int dst_stride,
+template <class E, bool BWD>
+__global__ __launch_bounds__(256) void rope_kernel(const typename E::T* __restrict__ src, int src_stride,
+                                                   typename E::T* __restrict__ dst, int dst_stride,
                                                    const float* __restrict__ cos_t,
                                                    const float* __restrict__ sin_t, int T, int S,
                                                    int width, int half_d) {
@@ -34,7 +34,7 @@ __global__ __launch_bounds__(256) void rope_kernel(const bf16_t* __restrict__ sr
     const float4 c = *reinterpret_cast<const float4*>(cos_t + (long)pos * half_d + fi);
     const float4 s = *reinterpret_cast<const float4*>(sin_t + (long)pos * half_d + fi);
     float x[8], y[8];
-    unpack8(*reinterpret_cast<const uint4*>(src + (long)row * src_stride + col), x);
+    ld8<E>(src + (long)row * src_stride + col, x);
     const float cc[4] = {c.x, c.y, c.z, c.w};
     const float ss[4] = {BWD ? -s.x : s.x, BWD ? -s.y : s.y, BWD ? -s.z : s.z, BWD ? -s.w : s.w};
 #pragma unroll
@@ -43,7 +43,7 @@ __global__ __launch_bounds__(256) void rope_kernel(const bf16_t* __restrict__ sr
       y[2 * p] = a * cc[p] - b * ss[p];
       y[2 * p + 1] = a * ss[p] + b * cc[p];
     }
-    *reinterpret_cast<uint4*>(dst + (long)row * dst_stride + col) = pack8(y);
+    st8<E>(dst + (long)row * dst_stride + col, y);
   }
 }
 
@@ -58,7 +58,7 @@ int grid_for(long work) {
 at::Tensor rope_fwd(const at::Tensor& qkv, const at::Tensor& cos_t, const at::Tensor& sin_t,
                     int64_t seq_len, int64_t hq, int64_t hkv, int64_t d) {
   FT_CHECK_CUDA(qkv);
-  FT_CHECK_BF16(qkv);
+  FT_CHECK_MODEL_DTYPE(qkv);
   FT_CHECK_CONTIG(qkv);
   FT_CHECK_F32(cos_t);
   FT_CHECK_F32(sin_t);
@@ -73,9 +73,10 @@ at::Tensor rope_fwd(const at::Tensor& qkv, const at::Tensor& cos_t, const at::Te
   auto out = at::empty({T, width}, qkv.options());
   const long work = (long)T * (width / 8);
   if (work > 0)
-    hipLaunchKernelGGL(rope_kernel<false>, dim3(grid_for(work)), dim3(256), 0, ft_stream(),
-                       cptr<bf16_t>(qkv), W, mptr<bf16_t>(out), width, cptr<float>(cos_t),
-                       cptr<float>(sin_t), T, (int)seq_len, width, (int)(d / 2));
+    FT_DISPATCH_E(qkv.scalar_type(),
+                  hipLaunchKernelGGL((rope_kernel<E, false>), dim3(grid_for(work)), dim3(256), 0, ft_stream(),
+                                     cptr<typename E::T>(qkv), W, mptr<typename E::T>(out), width,
+                                     cptr<float>(cos_t), cptr<float>(sin_t), T, (int)seq_len, width, (int)(d / 2)));
   FT_LAUNCH_CHECK();
   return out;
 }
@@ -84,7 +85,7 @@ at::Tensor rope_fwd(const at::Tensor& qkv, const at::Tensor& cos_t, const at::Te
 void rope_bwd_(const at::Tensor& dqkv, const at::Tensor& cos_t, const at::Tensor& sin_t,
                int64_t seq_len, int64_t hq, int64_t hkv, int64_t d) {
   FT_CHECK_CUDA(dqkv);
-  FT_CHECK_BF16(dqkv);
+  FT_CHECK_MODEL_DTYPE(dqkv);
   FT_CHECK_CONTIG(dqkv);
   const int W = (hq + 2 * hkv) * d;
   TORCH_CHECK(dqkv.size(-1) == W, "rope_bwd: width mismatch");
@@ -93,9 +94,10 @@ void rope_bwd_(const at::Tensor& dqkv, const at::Tensor& cos_t, const at::Tensor
   const at::DeviceGuard guard(dqkv.device());
   const long work = (long)T * (width / 8);
   if (work > 0)
-    hipLaunchKernelGGL(rope_kernel<true>, dim3(grid_for(work)), dim3(256), 0, ft_stream(),
-                       cptr<bf16_t>(dqkv), W, mptr<bf16_t>(dqkv), W, cptr<float>(cos_t),
-                       cptr<float>(sin_t), T, (int)seq_len, width, (int)(d / 2));
+    FT_DISPATCH_E(dqkv.scalar_type(),
+                  hipLaunchKernelGGL((rope_kernel<E, true>), dim3(grid_for(work)), dim3(256), 0, ft_stream(),
+                                     cptr<typename E::T>(dqkv), W, mptr<typename E::T>(dqkv), W,
+                                     cptr<float>(cos_t), cptr<float>(sin_t), T, (int)seq_len, width, (int)(d / 2)));
   FT_LAUNCH_CHECK();
 }
 

@@ -4,16 +4,18 @@
 // projections run as ONE GEMM against the concatenated [w1; w3] weight (they
 // are adjacent in the flat parameter buffer), so this kernel reads gu =
 // [T, 2F] (gate in columns [0,F), up in [F,2F)) and writes a = silu(g) * u.
-// fp32 math, one bf16 rounding per output (the reference rounds twice).
-// 16-B vector accesses, grid-stride.
+// fp32 math, one rounding per output (the reference rounds twice). bf16 / fp16 / fp32
+// (--model-dtype); 16-B (32-B for fp32) vector accesses, grid-stride. The tiled variants
+// that also write the transposed outputs are bf16 (the default model dtype's dW layout).
 #include "torch_utils.h"
 
 namespace {
 
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }
 
-__global__ __launch_bounds__(256) void swiglu_fwd_kernel(const bf16_t* __restrict__ gu,
-                                                         bf16_t* __restrict__ a, long T, int F) {
+template <class E>
+__global__ __launch_bounds__(256) void swiglu_fwd_kernel(const typename E::T* __restrict__ gu,
+                                                         typename E::T* __restrict__ a, long T, int F) {
   const int vpr = F >> 3;
   const long total = T * vpr;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
@@ -21,17 +23,18 @@ __global__ __launch_bounds__(256) void swiglu_fwd_kernel(const bf16_t* __restric
     const long row = i / vpr;
     const int col = (int)(i - row * vpr) * 8;
     float g[8], u[8], o[8];
-    unpack8(*reinterpret_cast<const uint4*>(gu + row * 2 * F + col), g);
-    unpack8(*reinterpret_cast<const uint4*>(gu + row * 2 * F + F + col), u);
+    ld8<E>(gu + row * 2 * F + col, g);
+    ld8<E>(gu + row * 2 * F + F + col, u);
 #pragma unroll
     for (int j = 0; j < 8; ++j) o[j] = g[j] * sigmoidf_(g[j]) * u[j];
-    *reinterpret_cast<uint4*>(a + row * F + col) = pack8(o);
+    st8<E>(a + row * F + col, o);
   }
 }
 
-__global__ __launch_bounds__(256) void swiglu_bwd_kernel(const bf16_t* __restrict__ da,
-                                                         const bf16_t* __restrict__ gu,
-                                                         bf16_t* __restrict__ dgu, long T, int F) {
+template <class E>
+__global__ __launch_bounds__(256) void swiglu_bwd_kernel(const typename E::T* __restrict__ da,
+                                                         const typename E::T* __restrict__ gu,
+                                                         typename E::T* __restrict__ dgu, long T, int F) {
   const int vpr = F >> 3;
   const long total = T * vpr;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
@@ -39,9 +42,9 @@ __global__ __launch_bounds__(256) void swiglu_bwd_kernel(const bf16_t* __restric
     const long row = i / vpr;
     const int col = (int)(i - row * vpr) * 8;
     float g[8], u[8], d[8], dg[8], du[8];
-    unpack8(*reinterpret_cast<const uint4*>(gu + row * 2 * F + col), g);
-    unpack8(*reinterpret_cast<const uint4*>(gu + row * 2 * F + F + col), u);
-    unpack8(*reinterpret_cast<const uint4*>(da + row * F + col), d);
+    ld8<E>(gu + row * 2 * F + col, g);
+    ld8<E>(gu + row * 2 * F + F + col, u);
+    ld8<E>(da + row * F + col, d);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const float s = sigmoidf_(g[j]);
@@ -49,8 +52,8 @@ __global__ __launch_bounds__(256) void swiglu_bwd_kernel(const bf16_t* __restric
       du[j] = d[j] * silu;
       dg[j] = d[j] * u[j] * (s + silu * (1.f - s));
     }
-    *reinterpret_cast<uint4*>(dgu + row * 2 * F + col) = pack8(dg);
-    *reinterpret_cast<uint4*>(dgu + row * 2 * F + F + col) = pack8(du);
+    st8<E>(dgu + row * 2 * F + col, dg);
+    st8<E>(dgu + row * 2 * F + F + col, du);
   }
 }
 
@@ -164,7 +167,7 @@ int grid_for(long work) {
 
 at::Tensor swiglu_fwd(const at::Tensor& gu) {
   FT_CHECK_CUDA(gu);
-  FT_CHECK_BF16(gu);
+  FT_CHECK_MODEL_DTYPE(gu);
   FT_CHECK_CONTIG(gu);
   const int F2 = gu.size(-1);
   TORCH_CHECK(F2 % 16 == 0, "swiglu: 2F must be a multiple of 16");
@@ -176,15 +179,17 @@ at::Tensor swiglu_fwd(const at::Tensor& gu) {
   auto a = at::empty(sizes, gu.options());
   const long work = T * (F / 8);
   if (work > 0)
-    hipLaunchKernelGGL(swiglu_fwd_kernel, dim3(grid_for(work)), dim3(256), 0, ft_stream(),
-                       cptr<bf16_t>(gu), mptr<bf16_t>(a), T, F);
+    FT_DISPATCH_E(gu.scalar_type(),
+                  hipLaunchKernelGGL(swiglu_fwd_kernel<E>, dim3(grid_for(work)), dim3(256), 0, ft_stream(),
+                                     cptr<typename E::T>(gu), mptr<typename E::T>(a), T, F));
   FT_LAUNCH_CHECK();
   return a;
 }
 
 at::Tensor swiglu_bwd(const at::Tensor& da, const at::Tensor& gu) {
   FT_CHECK_CUDA(da);
-  FT_CHECK_BF16(da);
+  FT_CHECK_MODEL_DTYPE(da);
+  TORCH_CHECK(da.scalar_type() == gu.scalar_type(), "swiglu_bwd: dtype mismatch");
   FT_CHECK_CONTIG(da);
   FT_CHECK_CONTIG(gu);
   const int F2 = gu.size(-1);
@@ -195,8 +200,10 @@ at::Tensor swiglu_bwd(const at::Tensor& da, const at::Tensor& gu) {
   auto dgu = at::empty_like(gu);
   const long work = T * (F / 8);
   if (work > 0)
-    hipLaunchKernelGGL(swiglu_bwd_kernel, dim3(grid_for(work)), dim3(256), 0, ft_stream(),
-                       cptr<bf16_t>(da), cptr<bf16_t>(gu), mptr<bf16_t>(dgu), T, F);
+    FT_DISPATCH_E(gu.scalar_type(),
+                  hipLaunchKernelGGL(swiglu_bwd_kernel<E>, dim3(grid_for(work)), dim3(256), 0, ft_stream(),
+                                     cptr<typename E::T>(da), cptr<typename E::T>(gu), mptr<typename E::T>(dgu),
+                                     T, F));
   FT_LAUNCH_CHECK();
   return dgu;
 }

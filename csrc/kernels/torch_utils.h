@@ -19,6 +19,30 @@ static inline hipStream_t ft_stream() {
 
 #define FT_LAUNCH_CHECK() FT_HIP_CHECK(hipGetLastError())
 
+// model dtypes with hand-written kernels: bf16 (default), fp16, fp32
+#define FT_CHECK_MODEL_DTYPE(t)                                                                           \
+  TORCH_CHECK((t).scalar_type() == at::kBFloat16 || (t).scalar_type() == at::kHalf ||                   \
+                  (t).scalar_type() == at::kFloat,                                                      \
+              #t " must be bf16, fp16 or fp32")
+
+// Runs BODY with E = the element type of scalar type ST (EBF16 / EF16 / EF32).
+#define FT_DISPATCH_E(ST, ...)                   \
+  do {                                           \
+    const auto _st = (ST);                       \
+    if (_st == at::kBFloat16) {                  \
+      using E = EBF16;                           \
+      __VA_ARGS__;                               \
+    } else if (_st == at::kHalf) {               \
+      using E = EF16;                            \
+      __VA_ARGS__;                               \
+    } else if (_st == at::kFloat) {              \
+      using E = EF32;                            \
+      __VA_ARGS__;                               \
+    } else {                                     \
+      TORCH_CHECK(false, "unsupported dtype ", _st); \
+    }                                            \
+  } while (0)
+
 template <typename T>
 static inline const T* cptr(const at::Tensor& t) {
   return reinterpret_cast<const T*>(t.data_ptr());

@@ -1,4 +1,4 @@
-// Fused vocabulary cross-entropy, forward + backward, on bf16 logits.
+// Fused vocabulary cross-entropy, forward + backward, on bf16 (fp16 / fp32) logits.
 //
 // Parity: reference train.py:101-102
 //   loss = cross_entropy(logits.flatten(0,1).float(), labels, reduction="sum") / num_items
@@ -14,17 +14,18 @@ namespace {
 
 constexpr float LOG2E = 1.4426950408889634f;
 
-__global__ __launch_bounds__(256) void xent_fwd_kernel(const bf16_t* __restrict__ logits,
+template <class E>
+__global__ __launch_bounds__(256) void xent_fwd_kernel(const typename E::T* __restrict__ logits,
                                                        const int64_t* __restrict__ labels,
                                                        float* __restrict__ loss,
                                                        float* __restrict__ lse, int V,
                                                        int ignore_index) {
   const int row = blockIdx.x;
-  const bf16_t* lr = logits + (long)row * V;
+  const typename E::T* lr = logits + (long)row * V;
   float m = -INFINITY, s = 0.f;
   for (int c = threadIdx.x * 8; c < V; c += 256 * 8) {
     float x[8];
-    unpack8(*reinterpret_cast<const uint4*>(lr + c), x);
+    ld8<E>(lr + c, x);
     float lm = x[0];
 #pragma unroll
     for (int j = 1; j < 8; ++j) lm = fmaxf(lm, x[j]);
@@ -59,12 +60,13 @@ __global__ __launch_bounds__(256) void xent_fwd_kernel(const bf16_t* __restrict_
     const float l = M + logf(S);
     lse[row] = l;
     const int64_t y = labels[row];
-    loss[row] = (y == ignore_index) ? 0.f : (l - bf2f(lr[y]));
+    loss[row] = (y == ignore_index) ? 0.f : (l - ld1<E>(lr + y));
   }
 }
 
 // dlogits in place: (exp(x - lse) - [j == y]) * scale, scale = grad * inv_count.
-__global__ __launch_bounds__(256) void xent_bwd_kernel(bf16_t* __restrict__ logits,
+template <class E>
+__global__ __launch_bounds__(256) void xent_bwd_kernel(typename E::T* __restrict__ logits,
                                                        const int64_t* __restrict__ labels,
                                                        const float* __restrict__ lse,
                                                        const float* __restrict__ grad,
@@ -73,35 +75,36 @@ __global__ __launch_bounds__(256) void xent_bwd_kernel(bf16_t* __restrict__ logi
   // rows grid-strided over y (gridDim.y is capped below 65536; long-context T exceeds it)
   for (int row = blockIdx.y; row < T; row += gridDim.y) {
     const int64_t y = labels[row];
-    bf16_t* lr = logits + (long)row * V;
+    typename E::T* lr = logits + (long)row * V;
     const float scale = (y == ignore_index) ? 0.f : grad[0] * inv_count[0];
     const float l = lse[row];
     for (int c = (blockIdx.x * 256 + threadIdx.x) * 8; c < V; c += gridDim.x * 256 * 8) {
       float x[8];
-      unpack8(*reinterpret_cast<const uint4*>(lr + c), x);
+      ld8<E>(lr + c, x);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         float p = exp2f((x[j] - l) * LOG2E);
         if (c + j == y) p -= 1.f;
         x[j] = p * scale;
       }
-      *reinterpret_cast<uint4*>(lr + c) = pack8(x);
+      st8<E>(lr + c, x);
     }
   }
 }
 
 // x *= g[0] unless g[0] == 1 (then every block exits at once): the upstream gradient of a
 // loss whose input gradients were already formed in the forward pass (fused LM head).
-__global__ __launch_bounds__(256) void scale_by_kernel(bf16_t* __restrict__ x, long n8,
+template <class E>
+__global__ __launch_bounds__(256) void scale_by_kernel(typename E::T* __restrict__ x, long n8,
                                                        const float* __restrict__ g) {
   const float s = g[0];
   if (s == 1.f) return;
   for (long i = blockIdx.x * 256L + threadIdx.x; i < n8; i += (long)gridDim.x * 256) {
     float v[8];
-    unpack8(reinterpret_cast<const uint4*>(x)[i], v);
+    ld8<E>(x + i * 8, v);
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[j] *= s;
-    reinterpret_cast<uint4*>(x)[i] = pack8(v);
+    st8<E>(x + i * 8, v);
   }
 }
 
@@ -109,15 +112,16 @@ __global__ __launch_bounds__(256) void scale_by_kernel(bf16_t* __restrict__ x, l
 
 void scale_by_(const at::Tensor& x, const at::Tensor& g) {
   FT_CHECK_CUDA(x);
-  FT_CHECK_BF16(x);
+  FT_CHECK_MODEL_DTYPE(x);
   FT_CHECK_CONTIG(x);
   FT_CHECK_F32(g);
   TORCH_CHECK(x.numel() % 8 == 0, "scale_by_: numel must be a multiple of 8");
   const at::DeviceGuard guard(x.device());
   const long n8 = x.numel() / 8;
   if (n8 > 0)
-    hipLaunchKernelGGL(scale_by_kernel, dim3((unsigned)std::min<long>((n8 + 255) / 256, 2048)), dim3(256), 0,
-                       ft_stream(), mptr<bf16_t>(x), n8, cptr<float>(g));
+    FT_DISPATCH_E(x.scalar_type(),
+                  hipLaunchKernelGGL(scale_by_kernel<E>, dim3((unsigned)std::min<long>((n8 + 255) / 256, 2048)),
+                                     dim3(256), 0, ft_stream(), mptr<typename E::T>(x), n8, cptr<float>(g)));
   FT_LAUNCH_CHECK();
 }
 
@@ -125,7 +129,7 @@ void scale_by_(const at::Tensor& x, const at::Tensor& g) {
 std::tuple<at::Tensor, at::Tensor> xent_fwd(const at::Tensor& logits, const at::Tensor& labels,
                                             int64_t ignore_index) {
   FT_CHECK_CUDA(logits);
-  FT_CHECK_BF16(logits);
+  FT_CHECK_MODEL_DTYPE(logits);
   FT_CHECK_CONTIG(logits);
   FT_CHECK_CONTIG(labels);
   TORCH_CHECK(labels.scalar_type() == at::kLong, "xent: labels must be int64");
@@ -137,9 +141,10 @@ std::tuple<at::Tensor, at::Tensor> xent_fwd(const at::Tensor& logits, const at::
   auto loss = at::empty({T}, logits.options().dtype(at::kFloat));
   auto lse = at::empty({T}, logits.options().dtype(at::kFloat));
   if (T > 0)
-    hipLaunchKernelGGL(xent_fwd_kernel, dim3(T), dim3(256), 0, ft_stream(), cptr<bf16_t>(logits),
-                       cptr<int64_t>(labels), mptr<float>(loss), mptr<float>(lse), V,
-                       (int)ignore_index);
+    FT_DISPATCH_E(logits.scalar_type(),
+                  hipLaunchKernelGGL(xent_fwd_kernel<E>, dim3(T), dim3(256), 0, ft_stream(),
+                                     cptr<typename E::T>(logits), cptr<int64_t>(labels), mptr<float>(loss),
+                                     mptr<float>(lse), V, (int)ignore_index));
   FT_LAUNCH_CHECK();
   return {loss, lse};
 }
@@ -148,7 +153,7 @@ std::tuple<at::Tensor, at::Tensor> xent_fwd(const at::Tensor& logits, const at::
 void xent_bwd_(const at::Tensor& logits, const at::Tensor& labels, const at::Tensor& lse,
                const at::Tensor& grad, const at::Tensor& inv_count, int64_t ignore_index) {
   FT_CHECK_CUDA(logits);
-  FT_CHECK_BF16(logits);
+  FT_CHECK_MODEL_DTYPE(logits);
   FT_CHECK_CONTIG(logits);
   FT_CHECK_F32(grad);
   FT_CHECK_F32(inv_count);
@@ -157,9 +162,10 @@ void xent_bwd_(const at::Tensor& logits, const at::Tensor& labels, const at::Ten
   const at::DeviceGuard guard(logits.device());
   const int bx = std::max(1, std::min((V / 8 + 255) / 256, 8));
   if (T > 0)
-    hipLaunchKernelGGL(xent_bwd_kernel, dim3(bx, std::min(T, 32768)), dim3(256), 0, ft_stream(),
-                       mptr<bf16_t>(logits), cptr<int64_t>(labels), cptr<float>(lse),
-                       cptr<float>(grad), cptr<float>(inv_count), V, T, (int)ignore_index);
+    FT_DISPATCH_E(logits.scalar_type(),
+                  hipLaunchKernelGGL(xent_bwd_kernel<E>, dim3(bx, std::min(T, 32768)), dim3(256), 0, ft_stream(),
+                                     mptr<typename E::T>(logits), cptr<int64_t>(labels), cptr<float>(lse),
+                                     cptr<float>(grad), cptr<float>(inv_count), V, T, (int)ignore_index));
   FT_LAUNCH_CHECK();
 }
 
