@@ -83,41 +83,114 @@ __device__ __forceinline__ typename E::T cvt1(float f) {
   else return f;
 }
 
+// 8 elements kept packed in registers (one uint4 for the 16-bit types, two for fp32):
+// kernels that hold whole rows between passes keep them packed and unpack per pass.
 template <class E>
-__device__ __forceinline__ void ld8(const typename E::T* p, float* f) {
+struct P8 {
+  uint4 v[E::is16 ? 1 : 2];
+};
+
+template <class E>
+__device__ __forceinline__ P8<E> ldp8(const typename E::T* p) {
+  P8<E> r;
+  r.v[0] = *reinterpret_cast<const uint4*>(p);
+  if constexpr (!E::is16) r.v[1] = *reinterpret_cast<const uint4*>(p + 4);
+  return r;
+}
+
+template <class E>
+__device__ __forceinline__ P8<E> zp8() {
+  P8<E> r;
+#pragma unroll
+  for (int i = 0; i < (E::is16 ? 1 : 2); ++i) r.v[i] = make_uint4(0, 0, 0, 0);
+  return r;
+}
+
+// Opaque register barrier: keeps the packed values (not their fp32 unpack) live.
+template <class E>
+__device__ __forceinline__ void pin8(P8<E>& r) {
+#pragma unroll
+  for (int i = 0; i < (E::is16 ? 1 : 2); ++i)
+    asm volatile("" : "+v"(r.v[i].x), "+v"(r.v[i].y), "+v"(r.v[i].z), "+v"(r.v[i].w));
+}
+
+template <class E>
+__device__ __forceinline__ void unp8(const P8<E>& r, float* f) {
   if constexpr (std::is_same<E, EBF16>::value) {
-    unpack8(*reinterpret_cast<const uint4*>(p), f);
+    unpack8(r.v[0], f);
   } else if constexpr (std::is_same<E, EF16>::value) {
-    const uint4 v = *reinterpret_cast<const uint4*>(p);
-    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    const uint32_t w[4] = {r.v[0].x, r.v[0].y, r.v[0].z, r.v[0].w};
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       f[2 * i] = h2f((uint16_t)(w[i] & 0xffffu));
       f[2 * i + 1] = h2f((uint16_t)(w[i] >> 16));
     }
   } else {
-    const float4 a = *reinterpret_cast<const float4*>(p);
-    const float4 b = *reinterpret_cast<const float4*>(p + 4);
-    f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w;
-    f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
+    f[0] = __uint_as_float(r.v[0].x); f[1] = __uint_as_float(r.v[0].y);
+    f[2] = __uint_as_float(r.v[0].z); f[3] = __uint_as_float(r.v[0].w);
+    f[4] = __uint_as_float(r.v[1].x); f[5] = __uint_as_float(r.v[1].y);
+    f[6] = __uint_as_float(r.v[1].z); f[7] = __uint_as_float(r.v[1].w);
+  }
+}
+
+// Round through the model dtype (identity for fp32).
+template <class E>
+__device__ __forceinline__ float rnd(float f) {
+  if constexpr (std::is_same<E, EF32>::value) return f;
+  else {
+    const typename E::T t = cvt1<E>(f);
+    return ld1<E>(&t);
   }
 }
 
 template <class E>
-__device__ __forceinline__ void st8(typename E::T* p, const float* f) {
+__device__ __forceinline__ void ld8(const typename E::T* p, float* f) {
+  unp8<E>(ldp8<E>(p), f);
+}
+
+template <class E>
+__device__ __forceinline__ P8<E> pk8(const float* f) {
+  P8<E> r;
   if constexpr (std::is_same<E, EBF16>::value) {
-    *reinterpret_cast<uint4*>(p) = pack8(f);
+    r.v[0] = pack8(f);
   } else if constexpr (std::is_same<E, EF16>::value) {
-    uint4 v;
-    v.x = (uint32_t)f2h(f[0]) | ((uint32_t)f2h(f[1]) << 16);
-    v.y = (uint32_t)f2h(f[2]) | ((uint32_t)f2h(f[3]) << 16);
-    v.z = (uint32_t)f2h(f[4]) | ((uint32_t)f2h(f[5]) << 16);
-    v.w = (uint32_t)f2h(f[6]) | ((uint32_t)f2h(f[7]) << 16);
-    *reinterpret_cast<uint4*>(p) = v;
+    r.v[0].x = (uint32_t)f2h(f[0]) | ((uint32_t)f2h(f[1]) << 16);
+    r.v[0].y = (uint32_t)f2h(f[2]) | ((uint32_t)f2h(f[3]) << 16);
+    r.v[0].z = (uint32_t)f2h(f[4]) | ((uint32_t)f2h(f[5]) << 16);
+    r.v[0].w = (uint32_t)f2h(f[6]) | ((uint32_t)f2h(f[7]) << 16);
   } else {
-    *reinterpret_cast<float4*>(p) = make_float4(f[0], f[1], f[2], f[3]);
-    *reinterpret_cast<float4*>(p + 4) = make_float4(f[4], f[5], f[6], f[7]);
+    r.v[0] = make_uint4(__float_as_uint(f[0]), __float_as_uint(f[1]), __float_as_uint(f[2]),
+                        __float_as_uint(f[3]));
+    r.v[1] = make_uint4(__float_as_uint(f[4]), __float_as_uint(f[5]), __float_as_uint(f[6]),
+                        __float_as_uint(f[7]));
   }
+  return r;
+}
+
+template <class E>
+__device__ __forceinline__ void st8(typename E::T* p, const float* f) {
+  const P8<E> r = pk8<E>(f);
+  *reinterpret_cast<uint4*>(p) = r.v[0];
+  if constexpr (!E::is16) *reinterpret_cast<uint4*>(p + 4) = r.v[1];
+}
+
+// 16-bit element types: 8 values in one uint4 <-> 8 floats; 2 floats -> one packed pair.
+template <class E>
+__device__ __forceinline__ void unpack8e(const uint4& v, float* f) {
+  static_assert(E::is16, "16-bit element types only");
+  P8<E> r;
+  r.v[0] = v;
+  unp8<E>(r, f);
+}
+template <class E>
+__device__ __forceinline__ uint4 pack8e(const float* f) {
+  static_assert(E::is16, "16-bit element types only");
+  return pk8<E>(f).v[0];
+}
+template <class E>
+__device__ __forceinline__ uint32_t pk2(float lo, float hi) {
+  static_assert(E::is16, "16-bit element types only");
+  return (uint32_t)cvt1<E>(lo) | ((uint32_t)cvt1<E>(hi) << 16);
 }
 
 __device__ __forceinline__ float wave_sum(float v) {

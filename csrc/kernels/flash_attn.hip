@@ -87,17 +87,52 @@ __device__ __forceinline__ void glds16(const void* g, char* lds_base) {
                                    (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
 }
 
-template <int D>
-__device__ __forceinline__ bf16x8_t ld_row(const char* img, int r, int c) {
-  return *reinterpret_cast<const bf16x8_t*>(img + lds_off<D>(r, c));
+// Fragment types of the 16-bit model dtypes (bf16 default, fp16 under --model-dtype fp16):
+// the same 32x32x16 MFMA shape and ds_read_b64_tr_b16 transposed reads exist for both, so the
+// kernels below are written once over E and differ only in these four primitives.
+typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4_t __attribute__((ext_vector_type(4)));
+typedef __fp16 fp16x4_raw_t __attribute__((__vector_size__(4 * sizeof(__fp16))));
+typedef __attribute__((address_space(3))) fp16x4_raw_t lds_f16x4_t;
+
+template <class E>
+struct FA;
+template <>
+struct FA<EBF16> {
+  typedef bf16x8_t v8;
+  typedef bf16x4_t v4;
+  typedef __bf16 s;
+  __device__ static v4 tr(const char* p) {
+    return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)(p));
+  }
+  __device__ static f32x16_t mfma(v8 a, v8 b, f32x16_t c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+  }
+};
+template <>
+struct FA<EF16> {
+  typedef f16x8_t v8;
+  typedef f16x4_t v4;
+  typedef _Float16 s;
+  __device__ static v4 tr(const char* p) {
+    return __builtin_bit_cast(v4, __builtin_amdgcn_ds_read_tr16_b64_v4f16((lds_f16x4_t*)(p)));
+  }
+  __device__ static f32x16_t mfma(v8 a, v8 b, f32x16_t c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+  }
+};
+
+template <class E, int D>
+__device__ __forceinline__ typename FA<E>::v8 ld_row(const char* img, int r, int c) {
+  return *reinterpret_cast<const typename FA<E>::v8*>(img + lds_off<D>(r, c));
 }
 
-__device__ __forceinline__ bf16x4_t ds_tr(const char* p) {
-  return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)(p));
-}
-
-__device__ __forceinline__ bf16x8_t cat8(bf16x4_t a, bf16x4_t b) {
-  bf16x8_t r;
+template <class V4>
+__device__ __forceinline__ auto cat8(V4 a, V4 b) {
+  typedef decltype(a[0]) S_;
+  typedef std::remove_cv_t<std::remove_reference_t<S_>> S;
+  typedef S V8 __attribute__((ext_vector_type(8)));
+  V8 r;
   r[0] = a[0]; r[1] = a[1]; r[2] = a[2]; r[3] = a[3];
   r[4] = b[0]; r[5] = b[1]; r[6] = b[2]; r[7] = b[3];
   return r;
@@ -107,37 +142,49 @@ __device__ __forceinline__ bf16x8_t cat8(bf16x4_t a, bf16x4_t b) {
 // column col0 + (lane & 31) of rows row0 + 4*hi + (0..3) (elements 0..3) and
 // row0 + 8 + 4*hi + (0..3) (elements 4..7) — the k order of an MFMA operand
 // built from a 32x32 accumulator's registers 8s..8s+7.
-template <int D>
-__device__ __forceinline__ bf16x8_t tr_frag(const char* img, int row0, int col0, int lane) {
+template <class E, int D>
+__device__ __forceinline__ typename FA<E>::v8 tr_frag(const char* img, int row0, int col0, int lane) {
   const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3, hi = lane >> 5;
   const int col = col0 + 16 * (g & 1) + 4 * p;
   const int r = row0 + 4 * hi + q;
   const int sub = ((col >> 2) & 1) * 8;
-  const bf16x4_t a = ds_tr(img + lds_off<D>(r, col >> 3) + sub);
-  const bf16x4_t b = ds_tr(img + lds_off<D>(r + 8, col >> 3) + sub);
+  const auto a = FA<E>::tr(img + lds_off<D>(r, col >> 3) + sub);
+  const auto b = FA<E>::tr(img + lds_off<D>(r + 8, col >> 3) + sub);
   return cat8(a, b);
 }
 
 // Same for the unswizzled [keys][32 q] dS image (64-B rows; 4 rows = one bank row).
-__device__ __forceinline__ bf16x8_t tr_frag_ds(const char* img, int row0, int lane) {
+template <class E>
+__device__ __forceinline__ typename FA<E>::v8 tr_frag_ds(const char* img, int row0, int lane) {
   const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3, hi = lane >> 5;
   const int col = 16 * (g & 1) + 4 * p;
   const int r = row0 + 4 * hi + q;
-  const bf16x4_t a = ds_tr(img + r * 64 + col * 2);
-  const bf16x4_t b = ds_tr(img + (r + 8) * 64 + col * 2);
+  const auto a = FA<E>::tr(img + r * 64 + col * 2);
+  const auto b = FA<E>::tr(img + (r + 8) * 64 + col * 2);
   return cat8(a, b);
 }
 
-template <int OFF>
-__device__ __forceinline__ bf16x8_t cvt8(const f32x16_t& v) {
-  bf16x8_t r;
-  r[0] = (__bf16)v[OFF + 0]; r[1] = (__bf16)v[OFF + 1]; r[2] = (__bf16)v[OFF + 2]; r[3] = (__bf16)v[OFF + 3];
-  r[4] = (__bf16)v[OFF + 4]; r[5] = (__bf16)v[OFF + 5]; r[6] = (__bf16)v[OFF + 6]; r[7] = (__bf16)v[OFF + 7];
+template <class E, int OFF>
+__device__ __forceinline__ typename FA<E>::v8 cvt8(const f32x16_t& v) {
+  typedef typename FA<E>::s S;
+  typename FA<E>::v8 r;
+  r[0] = (S)v[OFF + 0]; r[1] = (S)v[OFF + 1]; r[2] = (S)v[OFF + 2]; r[3] = (S)v[OFF + 3];
+  r[4] = (S)v[OFF + 4]; r[5] = (S)v[OFF + 5]; r[6] = (S)v[OFF + 6]; r[7] = (S)v[OFF + 7];
   return r;
 }
 
 __device__ __forceinline__ f32x16_t mfma32(bf16x8_t a, bf16x8_t b, f32x16_t c) {
-  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+  return FA<EBF16>::mfma(a, b, c);
+}
+__device__ __forceinline__ f32x16_t mfma32(f16x8_t a, f16x8_t b, f32x16_t c) {
+  return FA<EF16>::mfma(a, b, c);
+}
+
+// Low 16 bits of `bits` as an E value -> float.
+template <class E>
+__device__ __forceinline__ float u16f(uint32_t bits) {
+  const bf16_t t = (bf16_t)(bits & 0xffffu);
+  return ld1<E>(&t);
 }
 
 // Raw v_exp_f32 (2^x): exp2f adds denormal range-reduction (cmp + cndmask + ldexp per
@@ -171,7 +218,7 @@ __device__ __forceinline__ void map_head(int hh, int Hq, int Hkv, int& h, int& k
 // softmax and K/V buffers, and merge (m, l, O) through LDS at the end. That halves the causal
 // critical path (the last query tile's sweep over all keys) and gives every SIMD two waves, so
 // one's softmax overlaps the other's MFMAs.
-template <int D, int NW = 4, int SPLIT = 1>
+template <class E, int D, int NW = 4, int SPLIT = 1>
 __global__ __launch_bounds__(64 * NW * SPLIT, 8 / (NW * SPLIT)) void flash_fwd_kernel(
     const bf16_t* __restrict__ qk, const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out,
     float* __restrict__ lse2, int B, int S, int Hq, int Hkv, float sl2, long ldqk_) {
@@ -208,12 +255,12 @@ __global__ __launch_bounds__(64 * NW * SPLIT, 8 / (NW * SPLIT)) void flash_fwd_k
   const bf16_t* Kg = qk + (long)b * S * ldqk + (long)(Hq + kvh) * D;
   const bf16_t* Vg = qkv + (long)b * S * ldv + (long)(Hq + Hkv + kvh) * D;
 
-  bf16x8_t qf[KS];
+  typename FA<E>::v8 qf[KS];
   {
     const long qr = min(qrow, S - 1);
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks)
-      qf[ks] = *reinterpret_cast<const bf16x8_t*>(Qg + qr * ldqk + ks * 16 + hi * 8);
+      qf[ks] = *reinterpret_cast<const typename FA<E>::v8*>(Qg + qr * ldqk + ks * 16 + hi * 8);
   }
 
   const int kend = min((qt + 1) * BM, S);
@@ -267,7 +314,7 @@ __global__ __launch_bounds__(64 * NW * SPLIT, 8 / (NW * SPLIT)) void flash_fwd_k
         if (!MASK || j == 0 || v1) {
 #pragma unroll
           for (int ks = 0; ks < KS; ++ks)
-            s[j] = mfma32(ld_row<D>(kb, j * 32 + l32, 2 * ks + hi), qf[ks], s[j]);
+            s[j] = mfma32(ld_row<E, D>(kb, j * 32 + l32, 2 * ks + hi), qf[ks], s[j]);
         }
       }
       // max over raw scores (the softmax scale is > 0), scale folded into one FMA below
@@ -310,19 +357,19 @@ __global__ __launch_bounds__(64 * NW * SPLIT, 8 / (NW * SPLIT)) void flash_fwd_k
           ls += p;
           s[j][r] = p;
         }
-      const bf16x8_t pb00 = cvt8<0>(s[0]), pb01 = cvt8<8>(s[0]);
-      const bf16x8_t pb10 = cvt8<0>(s[1]), pb11 = cvt8<8>(s[1]);
+      const typename FA<E>::v8 pb00 = cvt8<E, 0>(s[0]), pb01 = cvt8<E, 8>(s[0]);
+      const typename FA<E>::v8 pb10 = cvt8<E, 0>(s[1]), pb11 = cvt8<E, 8>(s[1]);
       l += ls;
 #pragma unroll
       for (int db = 0; db < NDB; ++db) {
-        o[db] = mfma32(tr_frag<D>(vb, 0, db * 32, lane), pb00, o[db]);
-        o[db] = mfma32(tr_frag<D>(vb, 16, db * 32, lane), pb01, o[db]);
+        o[db] = mfma32(tr_frag<E, D>(vb, 0, db * 32, lane), pb00, o[db]);
+        o[db] = mfma32(tr_frag<E, D>(vb, 16, db * 32, lane), pb01, o[db]);
       }
       if (!MASK || v1) {
 #pragma unroll
         for (int db = 0; db < NDB; ++db) {
-          o[db] = mfma32(tr_frag<D>(vb, 32, db * 32, lane), pb10, o[db]);
-          o[db] = mfma32(tr_frag<D>(vb, 48, db * 32, lane), pb11, o[db]);
+          o[db] = mfma32(tr_frag<E, D>(vb, 32, db * 32, lane), pb10, o[db]);
+          o[db] = mfma32(tr_frag<E, D>(vb, 48, db * 32, lane), pb11, o[db]);
         }
       }
     };
@@ -380,8 +427,8 @@ __global__ __launch_bounds__(64 * NW * SPLIT, 8 / (NW * SPLIT)) void flash_fwd_k
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         uint2 v;
-        v.x = pack2(o[db][4 * g + 0] * inv, o[db][4 * g + 1] * inv);
-        v.y = pack2(o[db][4 * g + 2] * inv, o[db][4 * g + 3] * inv);
+        v.x = pk2<E>(o[db][4 * g + 0] * inv, o[db][4 * g + 1] * inv);
+        v.y = pk2<E>(o[db][4 * g + 2] * inv, o[db][4 * g + 3] * inv);
         *reinterpret_cast<uint2*>(orow + db * 32 + 8 * g + 4 * hi) = v;
       }
     if (hi == 0) lse2[((long)b * Hq + h) * stat_stride(S) + qrow] = m + log2f(l);
@@ -390,7 +437,7 @@ __global__ __launch_bounds__(64 * NW * SPLIT, 8 / (NW * SPLIT)) void flash_fwd_k
 
 // ================================================================== backward
 // delta[b,h,q] = sum_d dO * O   (one 16-lane group per (q, h) row, 8 bf16 per lane step)
-template <int D>
+template <class E, int D>
 __global__ __launch_bounds__(256) void flash_bwd_pre_kernel(const bf16_t* __restrict__ dO,
                                                             const bf16_t* __restrict__ O,
                                                             float* __restrict__ delta, int B,
@@ -404,8 +451,8 @@ __global__ __launch_bounds__(256) void flash_bwd_pre_kernel(const bf16_t* __rest
     const bf16_t* c = O + row * D;
     for (int d = sub * 8; d < D; d += 128) {
       float x[8], y[8];
-      unpack8(*reinterpret_cast<const uint4*>(a + d), x);
-      unpack8(*reinterpret_cast<const uint4*>(c + d), y);
+      ld8<E>(a + d, x);
+      ld8<E>(c + d, y);
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc += x[j] * y[j];
     }
@@ -422,7 +469,7 @@ __global__ __launch_bounds__(256) void flash_bwd_pre_kernel(const bf16_t* __rest
 
 // DQ: 0 = dQ by fp32 atomics (default), 1 = no dQ stage (dK/dV only; a separate
 // deterministic dQ kernel follows), 2 = timing experiment: plain (racy) stores.
-template <int D, int DQ = 0>
+template <class E, int D, int DQ = 0>
 __global__ __launch_bounds__(256, 1) void flash_bwd_kernel(
     const bf16_t* __restrict__ dO, const bf16_t* __restrict__ qk, const bf16_t* __restrict__ qkv,
     const float* __restrict__ lse2, const float* __restrict__ delta, float* __restrict__ dq_acc,
@@ -472,13 +519,13 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_kernel(
           *reinterpret_cast<const uint4*>(Kg + key * ldqk + c * 8);
     }
   }
-  bf16x8_t vf[KS], kf[KS];
+  typename FA<E>::v8 vf[KS], kf[KS];
   {
     const long key = min(kw + l32, S - 1);
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
-      vf[ks] = *reinterpret_cast<const bf16x8_t*>(Vg + key * ldv + ks * 16 + hi * 8);
-      kf[ks] = *reinterpret_cast<const bf16x8_t*>(Kg + key * ldqk + ks * 16 + hi * 8);
+      vf[ks] = *reinterpret_cast<const typename FA<E>::v8*>(Vg + key * ldv + ks * 16 + hi * 8);
+      kf[ks] = *reinterpret_cast<const typename FA<E>::v8*>(Kg + key * ldqk + ks * 16 + hi * 8);
     }
   }
 
@@ -547,8 +594,8 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_kernel(
       for (int r = 0; r < 16; ++r) s[r] = dp[r] = 0.f;
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
-        s = mfma32(ld_row<D>(qi, l32, 2 * ks + hi), kf[ks], s);
-        dp = mfma32(ld_row<D>(di, l32, 2 * ks + hi), vf[ks], dp);
+        s = mfma32(ld_row<E, D>(qi, l32, 2 * ks + hi), kf[ks], s);
+        dp = mfma32(ld_row<E, D>(di, l32, 2 * ks + hi), vf[ks], dp);
       }
       // C layout: lane -> key (col), registers -> query rows
       static_for<4>([&](auto G) {
@@ -571,14 +618,14 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_kernel(
           s[r] = p;
         }
       });
-      const bf16x8_t pa[2] = {cvt8<0>(s), cvt8<8>(s)};
-      const bf16x8_t da[2] = {cvt8<0>(dp), cvt8<8>(dp)};
+      const typename FA<E>::v8 pa[2] = {cvt8<E, 0>(s), cvt8<E, 8>(s)};
+      const typename FA<E>::v8 da[2] = {cvt8<E, 0>(dp), cvt8<E, 8>(dp)};
 #pragma unroll
       for (int ss = 0; ss < 2; ++ss)
 #pragma unroll
         for (int db = 0; db < NDB; ++db) {
-          dv[db] = mfma32(pa[ss], tr_frag<D>(di, 16 * ss, db * 32, lane), dv[db]);
-          dk[db] = mfma32(da[ss], tr_frag<D>(qi, 16 * ss, db * 32, lane), dk[db]);
+          dv[db] = mfma32(pa[ss], tr_frag<E, D>(di, 16 * ss, db * 32, lane), dv[db]);
+          dk[db] = mfma32(da[ss], tr_frag<E, D>(qi, 16 * ss, db * 32, lane), dk[db]);
         }
       if constexpr (DQ != 1) {
         // dS -> LDS image [key][q] (4 x 8-B writes per lane) for the in-kernel dQ stage
@@ -586,8 +633,8 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_kernel(
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           uint2 v;
-          v.x = pack2(dp[4 * g + 0], dp[4 * g + 1]);
-          v.y = pack2(dp[4 * g + 2], dp[4 * g + 3]);
+          v.x = pk2<E>(dp[4 * g + 0], dp[4 * g + 1]);
+          v.y = pk2<E>(dp[4 * g + 2], dp[4 * g + 3]);
           *reinterpret_cast<uint2*>(row + (8 * g + 4 * hi) * 2) = v;
         }
       }
@@ -615,7 +662,7 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_kernel(
 #pragma unroll
         for (int k2 = 0; k2 < KPW / 16; ++k2) {
           const int kk = kbeg + 16 * k2;
-          acc = mfma32(tr_frag_ds(dsimg, kk, lane), tr_frag<D>(kimg, kk, qdb * 32, lane), acc);
+          acc = mfma32(tr_frag_ds<E>(dsimg, kk, lane), tr_frag<E, D>(kimg, kk, qdb * 32, lane), acc);
         }
         const int d = qdb * 32 + l32;
 #pragma unroll
@@ -647,8 +694,8 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_kernel(
       const int k = kw + (r & 3) + 8 * (r >> 2) + 4 * hi;
       if (k < S) {
         const long off = ((long)b * S + k) * ldo + (long)h * D + db * 32 + l32;
-        dk_part[off] = f2bf(dk[db][r] * scale);
-        dv_part[off] = f2bf(dv[db][r]);
+        dk_part[off] = cvt1<E>(dk[db][r] * scale);
+        dv_part[off] = cvt1<E>(dv[db][r]);
       }
     }
 }
@@ -664,7 +711,7 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_kernel(
 // SPLIT = 2: two half-blocks take alternate slice pairs of the same keys and add their dK / dV
 // partials through LDS at the end (fixed order: bit-reproducible), halving the longest
 // (first) key block's sweep.
-template <int D, int NW = 4, int SPLIT = 1>
+template <class E, int D, int NW = 4, int SPLIT = 1>
 __global__ __launch_bounds__(64 * NW * SPLIT, SPLIT == 1 ? 4 / NW : 8 / (NW * SPLIT)) void flash_bwd_dkdv2_kernel(
     const bf16_t* __restrict__ dO, const bf16_t* __restrict__ qk, const bf16_t* __restrict__ qkv,
     const float* __restrict__ lse2, const float* __restrict__ delta, bf16_t* __restrict__ dk_part,
@@ -695,13 +742,13 @@ __global__ __launch_bounds__(64 * NW * SPLIT, SPLIT == 1 ? 4 / NW : 8 / (NW * SP
   const float* lseg = lse2 + ((long)b * Hq + h) * stat_stride(S);
   const float* delg = delta + ((long)b * Hq + h) * stat_stride(S);
 
-  bf16x8_t vf[KS], kf[KS];
+  typename FA<E>::v8 vf[KS], kf[KS];
   {
     const long key = min(kw + l32, S - 1);
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
-      vf[ks] = *reinterpret_cast<const bf16x8_t*>(Vg + key * ldv + ks * 16 + hi * 8);
-      kf[ks] = *reinterpret_cast<const bf16x8_t*>(Kg + key * ldqk + ks * 16 + hi * 8);
+      vf[ks] = *reinterpret_cast<const typename FA<E>::v8*>(Vg + key * ldv + ks * 16 + hi * 8);
+      kf[ks] = *reinterpret_cast<const typename FA<E>::v8*>(Kg + key * ldqk + ks * 16 + hi * 8);
     }
   }
 
@@ -748,8 +795,8 @@ __global__ __launch_bounds__(64 * NW * SPLIT, SPLIT == 1 ? 4 / NW : 8 / (NW * SP
     for (int r = 0; r < 16; ++r) sv[r] = dpv[r] = 0.f;
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
-      sv = mfma32(ld_row<D>(qi, l32, 2 * ks + hi), kf[ks], sv);
-      dpv = mfma32(ld_row<D>(di, l32, 2 * ks + hi), vf[ks], dpv);
+      sv = mfma32(ld_row<E, D>(qi, l32, 2 * ks + hi), kf[ks], sv);
+      dpv = mfma32(ld_row<E, D>(di, l32, 2 * ks + hi), vf[ks], dpv);
     }
   };
   auto fin = [&](const char* sl, const int i, f32x16_t sv, f32x16_t dpv, auto MASKED)
@@ -781,14 +828,14 @@ __global__ __launch_bounds__(64 * NW * SPLIT, SPLIT == 1 ? 4 / NW : 8 / (NW * SP
         sv[r] = p;
       }
     });
-    const bf16x8_t pa[2] = {cvt8<0>(sv), cvt8<8>(sv)};
-    const bf16x8_t da[2] = {cvt8<0>(dpv), cvt8<8>(dpv)};
+    const typename FA<E>::v8 pa[2] = {cvt8<E, 0>(sv), cvt8<E, 8>(sv)};
+    const typename FA<E>::v8 da[2] = {cvt8<E, 0>(dpv), cvt8<E, 8>(dpv)};
 #pragma unroll
     for (int ss = 0; ss < 2; ++ss)
 #pragma unroll
       for (int db = 0; db < NDB; ++db) {
-        dv[db] = mfma32(pa[ss], tr_frag<D>(di, 16 * ss, db * 32, lane), dv[db]);
-        dk[db] = mfma32(da[ss], tr_frag<D>(qi, 16 * ss, db * 32, lane), dk[db]);
+        dv[db] = mfma32(pa[ss], tr_frag<E, D>(di, 16 * ss, db * 32, lane), dv[db]);
+        dk[db] = mfma32(da[ss], tr_frag<E, D>(qi, 16 * ss, db * 32, lane), dk[db]);
       }
   };
   // one slice, general case (inactive / masked / ragged)
@@ -877,8 +924,8 @@ __global__ __launch_bounds__(64 * NW * SPLIT, SPLIT == 1 ? 4 / NW : 8 / (NW * SP
       const int k = kw + (r & 3) + 8 * (r >> 2) + 4 * hi;
       if (k < S) {
         const long off = ((long)b * S + k) * ldkv + (long)h * D + db * 32 + l32;
-        dk_part[off] = f2bf(dk[db][r] * scale);
-        dv_part[off] = f2bf(dv[db][r]);
+        dk_part[off] = cvt1<E>(dk[db][r] * scale);
+        dv_part[off] = cvt1<E>(dv[db][r]);
       }
     }
 }
@@ -894,7 +941,7 @@ __global__ __launch_bounds__(64 * NW * SPLIT, SPLIT == 1 ? 4 / NW : 8 / (NW * SP
 // SPLIT = 2 (small grids, see flash_bwd): as the forward's key split, two half-blocks sweep
 // the even / odd key tiles of the same queries and add their dQ partials through LDS (in a
 // fixed order: still bit-reproducible).
-template <int D, int NW = 4, int SPLIT = 1>
+template <class E, int D, int NW = 4, int SPLIT = 1>
 __global__ __launch_bounds__(64 * NW * SPLIT, SPLIT == 1 ? 4 / NW : 8 / (NW * SPLIT)) void flash_bwd_dq_kernel(
     const bf16_t* __restrict__ dO, const bf16_t* __restrict__ qk, const bf16_t* __restrict__ qkv,
     const float* __restrict__ lse2, const float* __restrict__ delta, bf16_t* __restrict__ dqkv, int B,
@@ -929,12 +976,12 @@ __global__ __launch_bounds__(64 * NW * SPLIT, SPLIT == 1 ? 4 / NW : 8 / (NW * SP
   const bf16_t* Vg = qkv + (long)b * S * ldv + (long)(Hq + Hkv + kvh) * D;
   const bf16_t* dOg = dO + (long)b * S * ldo + (long)h * D;
 
-  bf16x8_t qf[KS], df[KS];
+  typename FA<E>::v8 qf[KS], df[KS];
   const long qr = min(qrow, S - 1);
 #pragma unroll
   for (int ks = 0; ks < KS; ++ks) {
-    qf[ks] = *reinterpret_cast<const bf16x8_t*>(Qg + qr * ldqk + ks * 16 + hi * 8);
-    df[ks] = *reinterpret_cast<const bf16x8_t*>(dOg + qr * ldo + ks * 16 + hi * 8);
+    qf[ks] = *reinterpret_cast<const typename FA<E>::v8*>(Qg + qr * ldqk + ks * 16 + hi * 8);
+    df[ks] = *reinterpret_cast<const typename FA<E>::v8*>(dOg + qr * ldo + ks * 16 + hi * 8);
   }
   const float lq = lse2[((long)b * Hq + h) * stat_stride(S) + qr];
   const float dlq = delta[((long)b * Hq + h) * stat_stride(S) + qr];
@@ -990,8 +1037,8 @@ __global__ __launch_bounds__(64 * NW * SPLIT, SPLIT == 1 ? 4 / NW : 8 / (NW * SP
         if (!MASK || j == 0 || v1) {
 #pragma unroll
           for (int ks = 0; ks < KS; ++ks) {
-            sc[j] = mfma32(ld_row<D>(kb, j * 32 + l32, 2 * ks + hi), qf[ks], sc[j]);
-            dp[j] = mfma32(ld_row<D>(vb, j * 32 + l32, 2 * ks + hi), df[ks], dp[j]);
+            sc[j] = mfma32(ld_row<E, D>(kb, j * 32 + l32, 2 * ks + hi), qf[ks], sc[j]);
+            dp[j] = mfma32(ld_row<E, D>(vb, j * 32 + l32, 2 * ks + hi), df[ks], dp[j]);
           }
         }
       }
@@ -1006,18 +1053,18 @@ __global__ __launch_bounds__(64 * NW * SPLIT, SPLIT == 1 ? 4 / NW : 8 / (NW * SP
           }
           sc[j][r] = p * (dp[j][r] - dlq);
         }
-      const bf16x8_t d00 = cvt8<0>(sc[0]), d01 = cvt8<8>(sc[0]);
-      const bf16x8_t d10 = cvt8<0>(sc[1]), d11 = cvt8<8>(sc[1]);
+      const typename FA<E>::v8 d00 = cvt8<E, 0>(sc[0]), d01 = cvt8<E, 8>(sc[0]);
+      const typename FA<E>::v8 d10 = cvt8<E, 0>(sc[1]), d11 = cvt8<E, 8>(sc[1]);
 #pragma unroll
       for (int db = 0; db < NDB; ++db) {
-        dq[db] = mfma32(tr_frag<D>(kb, 0, db * 32, lane), d00, dq[db]);
-        dq[db] = mfma32(tr_frag<D>(kb, 16, db * 32, lane), d01, dq[db]);
+        dq[db] = mfma32(tr_frag<E, D>(kb, 0, db * 32, lane), d00, dq[db]);
+        dq[db] = mfma32(tr_frag<E, D>(kb, 16, db * 32, lane), d01, dq[db]);
       }
       if (!MASK || v1) {
 #pragma unroll
         for (int db = 0; db < NDB; ++db) {
-          dq[db] = mfma32(tr_frag<D>(kb, 32, db * 32, lane), d10, dq[db]);
-          dq[db] = mfma32(tr_frag<D>(kb, 48, db * 32, lane), d11, dq[db]);
+          dq[db] = mfma32(tr_frag<E, D>(kb, 32, db * 32, lane), d10, dq[db]);
+          dq[db] = mfma32(tr_frag<E, D>(kb, 48, db * 32, lane), d11, dq[db]);
         }
       }
     };
@@ -1060,14 +1107,15 @@ __global__ __launch_bounds__(64 * NW * SPLIT, SPLIT == 1 ? 4 / NW : 8 / (NW * SP
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         uint2 v;
-        v.x = pack2(dq[db][4 * g + 0] * scale, dq[db][4 * g + 1] * scale);
-        v.y = pack2(dq[db][4 * g + 2] * scale, dq[db][4 * g + 3] * scale);
+        v.x = pk2<E>(dq[db][4 * g + 0] * scale, dq[db][4 * g + 1] * scale);
+        v.y = pk2<E>(dq[db][4 * g + 2] * scale, dq[db][4 * g + 3] * scale);
         *reinterpret_cast<uint2*>(orow + db * 32 + 8 * g + 4 * hi) = v;
       }
   }
 }
 
 // dqkv[:, q | k | v] = bf16(dQ), bf16(sum_G dK_part), bf16(sum_G dV_part)
+template <class E>
 __global__ __launch_bounds__(256) void flash_bwd_finalize_kernel(
     const float* __restrict__ dq_acc, const bf16_t* __restrict__ dk_part,
     const bf16_t* __restrict__ dv_part, bf16_t* __restrict__ dqkv, long T, int Hq, int Hkv, int D) {
@@ -1090,13 +1138,13 @@ __global__ __launch_bounds__(256) void flash_bwd_finalize_kernel(
       v = make_float4(0.f, 0.f, 0.f, 0.f);
       for (int r = 0; r < G; ++r) {
         const uint2 x = *reinterpret_cast<const uint2*>(src + r * D);
-        v.x += __uint_as_float(x.x << 16); v.y += __uint_as_float(x.x & 0xffff0000u);
-        v.z += __uint_as_float(x.y << 16); v.w += __uint_as_float(x.y & 0xffff0000u);
+        v.x += u16f<E>(x.x); v.y += u16f<E>(x.x >> 16);
+        v.z += u16f<E>(x.y); v.w += u16f<E>(x.y >> 16);
       }
     }
     uint2 o;
-    o.x = pack2(v.x, v.y);
-    o.y = pack2(v.z, v.w);
+    o.x = pk2<E>(v.x, v.y);
+    o.y = pk2<E>(v.z, v.w);
     *reinterpret_cast<uint2*>(dqkv + t * W + col) = o;
   }
 }
@@ -1151,8 +1199,9 @@ int waves_per_block(long S, long B, long Hq, long D) {
 void check_inputs(const at::Tensor& qk, const at::Tensor& qkv, int64_t S, int64_t Hq, int64_t Hkv,
                   int64_t D) {
   FT_CHECK_CUDA(qk);
-  FT_CHECK_BF16(qk);
-  FT_CHECK_BF16(qkv);
+  TORCH_CHECK(qk.scalar_type() == at::kBFloat16 || qk.scalar_type() == at::kHalf,
+              "flash: qk must be bf16 or fp16 (fp32 models use flash_f32_*)");
+  TORCH_CHECK(qkv.scalar_type() == qk.scalar_type(), "flash: qk / qkv dtype mismatch");
   FT_CHECK_CONTIG(qk);
   FT_CHECK_CONTIG(qkv);
   TORCH_CHECK(D == 64 || D == 128, "flash: head_dim must be 64 or 128");
@@ -1185,14 +1234,16 @@ std::tuple<at::Tensor, at::Tensor> flash_fwd(const at::Tensor& qk, const at::Ten
   const bool split = g_fwd_split >= 0 ? g_fwd_split == 1 : (long)nqt * B * Hq <= 256;
   dim3 grid(nqt * B * Hq), block(64 * nw * (split ? 2 : 1));
 #define FT_FWD(DD, SP)                                                                             \
-  hipLaunchKernelGGL((flash_fwd_kernel<DD, 4, SP>), grid, block, 0, ft_stream(), cptr<bf16_t>(qk), \
+  hipLaunchKernelGGL((flash_fwd_kernel<E, DD, 4, SP>), grid, block, 0, ft_stream(), cptr<bf16_t>(qk), \
                      cptr<bf16_t>(qkv), mptr<bf16_t>(out), mptr<float>(lse), B, (int)S, (int)Hq,   \
                      (int)Hkv, sl2, ldqk)
-  if (D == 128) {
-    if (split) FT_FWD(128, 2); else FT_FWD(128, 1);
-  } else {
-    if (split) FT_FWD(64, 2); else FT_FWD(64, 1);
-  }
+  FT_DISPATCH_E16(qk.scalar_type(), {
+    if (D == 128) {
+      if (split) FT_FWD(128, 2); else FT_FWD(128, 1);
+    } else {
+      if (split) FT_FWD(64, 2); else FT_FWD(64, 1);
+    }
+  });
 #undef FT_FWD
   FT_LAUNCH_CHECK();
   return {out, lse};
@@ -1241,7 +1292,7 @@ at::Tensor flash_bwd(const at::Tensor& dout, const at::Tensor& qk, const at::Ten
   const dim3 grid2(nkt2 * B * Hq), block2(64 * nw);
   float* dqp = det ? nullptr : mptr<float>(dq_acc);
 #define FT_BWD(DD, MODE)                                                                          \
-  hipLaunchKernelGGL((flash_bwd_kernel<DD, MODE>), grid, block, 0, ft_stream(), cptr<bf16_t>(dout), \
+  hipLaunchKernelGGL((flash_bwd_kernel<E, DD, MODE>), grid, block, 0, ft_stream(), cptr<bf16_t>(dout), \
                      cptr<bf16_t>(qk), cptr<bf16_t>(qkv), cptr<float>(lse), cptr<float>(delta),     \
                      dqp, dkp, dvp, B, (int)S, (int)Hq, (int)Hkv,                                    \
                      sl2, scale, ldqk)
@@ -1249,7 +1300,7 @@ at::Tensor flash_bwd(const at::Tensor& dout, const at::Tensor& qk, const at::Ten
   // forces; default: grids of at most one wave per SIMD
   const bool kv_split = D == 64 && (g_kv_split >= 0 ? g_kv_split == 1 : (long)grid2.x * nw <= 1024);
 #define FT_DKDV2(DD, NW_, SP_)                                                                             \
-  hipLaunchKernelGGL((flash_bwd_dkdv2_kernel<DD, NW_, SP_>), grid2, dim3(64 * NW_ * SP_), 0, ft_stream(), \
+  hipLaunchKernelGGL((flash_bwd_dkdv2_kernel<E, DD, NW_, SP_>), grid2, dim3(64 * NW_ * SP_), 0, ft_stream(), \
                      cptr<bf16_t>(dout), cptr<bf16_t>(qk), cptr<bf16_t>(qkv), cptr<float>(lse),           \
                      cptr<float>(delta), dkp, dvp, ldkv, B, (int)S,                                       \
                      (int)Hq, (int)Hkv, sl2, scale, ldqk)
@@ -1259,37 +1310,39 @@ at::Tensor flash_bwd(const at::Tensor& dout, const at::Tensor& qk, const at::Ten
   const bool dq_split = g_dq_split != 0;
 #define FT_DQ(DD, NW_)                                                                                  \
   if (dq_split)                                                                                         \
-    hipLaunchKernelGGL((flash_bwd_dq_kernel<DD, NW_, 2>), grid2, dim3(128 * NW_), 0, ft_stream(),       \
+    hipLaunchKernelGGL((flash_bwd_dq_kernel<E, DD, NW_, 2>), grid2, dim3(128 * NW_), 0, ft_stream(),       \
                        cptr<bf16_t>(dout), cptr<bf16_t>(qk), cptr<bf16_t>(qkv), cptr<float>(lse),       \
                        cptr<float>(delta), mptr<bf16_t>(dqkv), B, (int)S, (int)Hq, (int)Hkv, sl2, scale, ldqk); \
   else                                                                                                  \
-    hipLaunchKernelGGL((flash_bwd_dq_kernel<DD, NW_, 1>), grid2, block2, 0, ft_stream(),                \
+    hipLaunchKernelGGL((flash_bwd_dq_kernel<E, DD, NW_, 1>), grid2, block2, 0, ft_stream(),                \
                        cptr<bf16_t>(dout), cptr<bf16_t>(qk), cptr<bf16_t>(qkv), cptr<float>(lse),       \
                        cptr<float>(delta), mptr<bf16_t>(dqkv), B, (int)S, (int)Hq, (int)Hkv, sl2, scale, ldqk)
-  if (D == 128) {
-    hipLaunchKernelGGL(flash_bwd_pre_kernel<128>, dim3(pre_blocks), block, 0, ft_stream(),
-                       cptr<bf16_t>(dout), cptr<bf16_t>(out), mptr<float>(delta), B, (int)S, (int)Hq);
-    if (mode == 0) FT_BWD(128, 0);
-    else if (mode == 1) { if (g_dkdv2 && nw == 4) { FT_DKDV2(128, 4, 1); } else FT_BWD(128, 1); FT_DQ(128, 4); }
-    else FT_BWD(128, 2);
-  } else {
-    hipLaunchKernelGGL(flash_bwd_pre_kernel<64>, dim3(pre_blocks), block, 0, ft_stream(),
-                       cptr<bf16_t>(dout), cptr<bf16_t>(out), mptr<float>(delta), B, (int)S, (int)Hq);
-    if (mode == 0) FT_BWD(64, 0);
-    else if (mode == 1 && nw == 2) {
-      if (kv_split) FT_DKDV2(64, 2, 2); else FT_DKDV2(64, 2, 1);
-      FT_DQ(64, 2);
+  FT_DISPATCH_E16(qk.scalar_type(), {
+    if (D == 128) {
+      hipLaunchKernelGGL((flash_bwd_pre_kernel<E, 128>), dim3(pre_blocks), block, 0, ft_stream(),
+                         cptr<bf16_t>(dout), cptr<bf16_t>(out), mptr<float>(delta), B, (int)S, (int)Hq);
+      if (mode == 0) FT_BWD(128, 0);
+      else if (mode == 1) { if (g_dkdv2 && nw == 4) { FT_DKDV2(128, 4, 1); } else FT_BWD(128, 1); FT_DQ(128, 4); }
+      else FT_BWD(128, 2);
+    } else {
+      hipLaunchKernelGGL((flash_bwd_pre_kernel<E, 64>), dim3(pre_blocks), block, 0, ft_stream(),
+                         cptr<bf16_t>(dout), cptr<bf16_t>(out), mptr<float>(delta), B, (int)S, (int)Hq);
+      if (mode == 0) FT_BWD(64, 0);
+      else if (mode == 1 && nw == 2) {
+        if (kv_split) FT_DKDV2(64, 2, 2); else FT_DKDV2(64, 2, 1);
+        FT_DQ(64, 2);
+      }
+      // head_dim 64 with 4-wave blocks: the one-slice dK/dV kernel is faster (S = 8192, 16 heads:
+      // 631 vs 783 us, profiles/r2_flash_long_context.log); FT_FLASH_DKDV2=2 forces the slice pair
+      else if (mode == 1) {
+        if (g_dkdv2_64 && kv_split) FT_DKDV2(64, 4, 2);
+        else if (g_dkdv2_64) FT_DKDV2(64, 4, 1);
+        else FT_BWD(64, 1);
+        FT_DQ(64, 4);
+      }
+      else FT_BWD(64, 2);
     }
-    // head_dim 64 with 4-wave blocks: the one-slice dK/dV kernel is faster (S = 8192, 16 heads:
-    // 631 vs 783 us, profiles/r2_flash_long_context.log); FT_FLASH_DKDV2=2 forces the slice pair
-    else if (mode == 1) {
-      if (g_dkdv2_64 && kv_split) FT_DKDV2(64, 4, 2);
-      else if (g_dkdv2_64) FT_DKDV2(64, 4, 1);
-      else FT_BWD(64, 1);
-      FT_DQ(64, 4);
-    }
-    else FT_BWD(64, 2);
-  }
+  });
 #undef FT_BWD
 #undef FT_DKDV2
 #undef FT_DQ
@@ -1297,9 +1350,11 @@ at::Tensor flash_bwd(const at::Tensor& dout, const at::Tensor& qk, const at::Ten
   if (direct) return dqkv;
   const long vec = (long)T * ((Hq + 2 * Hkv) * D / 4);
   const int fin_blocks = (int)std::max(1L, std::min((vec + 255) / 256, 4096L));
-  hipLaunchKernelGGL(flash_bwd_finalize_kernel, dim3(fin_blocks), block, 0, ft_stream(),
-                     det ? nullptr : cptr<float>(dq_acc), cptr<bf16_t>(dk_part), cptr<bf16_t>(dv_part),
-                     mptr<bf16_t>(dqkv), (long)T, (int)Hq, (int)Hkv, (int)D);
+  FT_DISPATCH_E16(qk.scalar_type(),
+                  hipLaunchKernelGGL((flash_bwd_finalize_kernel<E>), dim3(fin_blocks), block, 0, ft_stream(),
+                                     det ? nullptr : cptr<float>(dq_acc), cptr<bf16_t>(dk_part),
+                                     cptr<bf16_t>(dv_part), mptr<bf16_t>(dqkv), (long)T, (int)Hq,
+                                     (int)Hkv, (int)D));
   FT_LAUNCH_CHECK();
   return dqkv;
 }

@@ -1,11 +1,11 @@
-// 4-wave bf16 GEMM for gfx950 with an instruction-level schedule (the "w4" kernel).
+// 4-wave bf16 / fp16 GEMM for gfx950 with an instruction-level schedule (the "w4" kernel).
 //
 //   C[M, N] = sum_k A(m, k) * B(k, n)   A = [M, K] row-major (K contiguous), B = [N, K] row-major
 //   (the forward x W^T of every nn.Linear: reference model.py:195,215,254,379)
 //
 // Structure (one workgroup = one 256 x BN output tile, BN = 32 * NJ, BK = 64):
 //   * 4 waves, one per SIMD, each owning a 128 x (16 NJ) quadrant = 8 x NJ fragments of
-//     v_mfma_f32_16x16x32_bf16; the accumulators are pinned in AGPRs (the MFMAs are inline asm on
+//     v_mfma_f32_16x16x32_bf16 (_f16 for --model-dtype fp16); the accumulators are pinned in AGPRs (the MFMAs are inline asm on
 //     "+a" operands, so the compiler never shuffles them), the operand fragments in VGPRs.
 //     NJ is chosen per shape so the tile count fills the 256 CUs in whole rounds (the 8B step:
 //     qkv 256 x 192 -> 256 tiles, w13 256 x 224 -> 4 x 256, wo / w2 256 x 128 -> 256, head 256^2).
@@ -87,8 +87,13 @@ __device__ __forceinline__ void ds16(bf16x8_t& d, unsigned addr) {
   asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(d) : "v"(addr), "i"(OFF) : "memory");
 }
 
+// bf16 or fp16 operands (--model-dtype): same shape, same schedule, another opcode
+template <class E>
 __device__ __forceinline__ void mfma(f32x4_t& c, const bf16x8_t& a, const bf16x8_t& b) {
-  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
+  if constexpr (std::is_same<E, EF16>::value)
+    asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
+  else
+    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
 }
 
 template <int N>
@@ -167,7 +172,7 @@ struct Ctx {
 
 // One K-tile t (stage cur = t & 1): DMA: stage tile t + 2 into this stage; NEXT: read tile t + 1's
 // first k-step.
-template <int NJ, bool DMA, bool NEXT>
+template <class E, int NJ, bool DMA, bool NEXT>
 __device__ __forceinline__ void ktile(f32x4_t (&acc)[8][NJ], Frags<NJ>& f, int t, const Ctx& c) {
   using S = Sched<NJ>;
   const unsigned cur = (unsigned)(t & 1) * S::ST, nxt = (unsigned)((t + 1) & 1) * S::ST;
@@ -188,9 +193,9 @@ __device__ __forceinline__ void ktile(f32x4_t (&acc)[8][NJ], Frags<NJ>& f, int t
     }
     if constexpr (s == 2) asm volatile("s_setprio 3" ::: "memory");
     if constexpr (s < S::MH)
-      mfma(acc[i][j], f.b0[j], f.a0[i]);
+      mfma<E>(acc[i][j], f.b0[j], f.a0[i]);
     else
-      mfma(acc[i][j], f.b1[j], f.a1[i]);
+      mfma<E>(acc[i][j], f.b1[j], f.a1[i]);
     if constexpr (s < S::R) rd<NJ, s>(f.a1, f.b1, a1b, b1b);
     if constexpr (s == S::SB1) {  // this stage fully read by every wave -> it may be restaged
       lgkm<0>();
@@ -225,7 +230,7 @@ __device__ __forceinline__ void ktile(f32x4_t (&acc)[8][NJ], Frags<NJ>& f, int t
   });
 }
 
-template <int NJ, int EPI>
+template <class E, int NJ, int EPI>
 __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(W4Args p) {
   using S = Sched<NJ>;
   constexpr int LDS = 2 * S::ST > 4 * 32768 ? 2 * S::ST : 4 * 32768;  // stages / epilogue staging
@@ -288,12 +293,12 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(W4Args p) {
   asm volatile("s_nop 4" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
   int t = 0;
-  for (; t + 2 < nk; ++t) ktile<NJ, true, true>(acc, f, t, c);
+  for (; t + 2 < nk; ++t) ktile<E, NJ, true, true>(acc, f, t, c);
   if (nk >= 2) {
-    ktile<NJ, false, true>(acc, f, t, c);
+    ktile<E, NJ, false, true>(acc, f, t, c);
     ++t;
   }
-  ktile<NJ, false, false>(acc, f, t, c);
+  ktile<E, NJ, false, false>(acc, f, t, c);
   // The accumulators are read by VALU next: wait out the last MFMAs (the compiler does not see
   // the asm as MFMAs, so it inserts no wait states), and keep every accumulator read behind the
   // pad (sched_barrier: register-only instructions may otherwise be hoisted above an asm).
@@ -314,8 +319,8 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(W4Args p) {
         const int ch = 2 * j + (hc >> 1);
         const f32x4_t v = acc[i][j];
         uint2 o;
-        o.x = pack2(v[0], v[1]);
-        o.y = pack2(v[2], v[3]);
+        o.x = pk2<E>(v[0], v[1]);
+        o.y = pk2<E>(v[2], v[3]);
         *reinterpret_cast<uint2*>(wl + m * 256 + ((ch ^ (m & 15)) << 4) + (hc & 1) * 8) = o;
       }
     }
@@ -332,11 +337,11 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(W4Args p) {
       const int gn = n0 + wn * NW + cc * 8;
       if constexpr (EPI == W4_RES) {
         float a[8], r[8];
-        unpack8(v, a);
-        unpack8(*reinterpret_cast<const uint4*>(p.r + gm * p.ldr + gn), r);
+        unpack8e<E>(v, a);
+        unpack8e<E>(*reinterpret_cast<const uint4*>(p.r + gm * p.ldr + gn), r);
 #pragma unroll
         for (int q = 0; q < 8; ++q) a[q] += r[q];
-        v = pack8(a);
+        v = pack8e<E>(a);
       } else if constexpr (EPI == W4_ROPE) {
         if (gn < p.rope_cols) {
           // 8 columns = 4 interleaved (x0, x1) pairs of one head: rotated in fp32 by the bf16
@@ -348,7 +353,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(W4Args p) {
           const float4 c4 = *reinterpret_cast<const float4*>(cs);
           const float4 s4 = *reinterpret_cast<const float4*>(sn);
           float a[8];
-          unpack8(v, a);
+          unpack8e<E>(v, a);
           const float cv[4] = {c4.x, c4.y, c4.z, c4.w}, sv[4] = {s4.x, s4.y, s4.z, s4.w};
           float o[8];
 #pragma unroll
@@ -356,7 +361,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(W4Args p) {
             o[2 * q] = a[2 * q] * cv[q] - a[2 * q + 1] * sv[q];
             o[2 * q + 1] = a[2 * q] * sv[q] + a[2 * q + 1] * cv[q];
           }
-          v = pack8(o);
+          v = pack8e<E>(o);
         }
       }
       *reinterpret_cast<uint4*>(p.c + gm * p.ldc + gn) = v;
@@ -364,15 +369,26 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(W4Args p) {
   }
 }
 
-template <int NJ>
+template <class E, int NJ>
 void launch_nj(const W4Args& p, int epi, hipStream_t st) {
   const dim3 g(p.tiles_m * p.tiles_n);
   if (epi == W4_RES)
-    hipLaunchKernelGGL((gemm_w4_kernel<NJ, W4_RES>), g, dim3(NT), 0, st, p);
+    hipLaunchKernelGGL((gemm_w4_kernel<E, NJ, W4_RES>), g, dim3(NT), 0, st, p);
   else if (epi == W4_ROPE)
-    hipLaunchKernelGGL((gemm_w4_kernel<NJ, W4_ROPE>), g, dim3(NT), 0, st, p);
+    hipLaunchKernelGGL((gemm_w4_kernel<E, NJ, W4_ROPE>), g, dim3(NT), 0, st, p);
   else
-    hipLaunchKernelGGL((gemm_w4_kernel<NJ, W4_STORE>), g, dim3(NT), 0, st, p);
+    hipLaunchKernelGGL((gemm_w4_kernel<E, NJ, W4_STORE>), g, dim3(NT), 0, st, p);
+}
+
+void launch(at::ScalarType st_, int nj, const W4Args& p, int epi, hipStream_t st) {
+  FT_DISPATCH_E16(st_, {
+    switch (nj) {
+      case 8: launch_nj<E, 8>(p, epi, st); break;
+      case 7: launch_nj<E, 7>(p, epi, st); break;
+      case 6: launch_nj<E, 6>(p, epi, st); break;
+      default: launch_nj<E, 4>(p, epi, st); break;
+    }
+  });
 }
 
 // Tile width for N: whole rounds of 256 tiles where possible (M = 2048 -> 8 row tiles).
@@ -403,8 +419,8 @@ int pick_nj(long M, long N) {
 at::Tensor gemm_nt_w4(const at::Tensor& a, const at::Tensor& b, const std::optional<at::Tensor>& out,
                       const std::optional<at::Tensor>& residual, int64_t nj) {
   FT_CHECK_CUDA(a);
-  FT_CHECK_BF16(a);
-  FT_CHECK_BF16(b);
+  TORCH_CHECK(a.scalar_type() == at::kBFloat16 || a.scalar_type() == at::kHalf, "gemm_nt_w4: bf16 / fp16");
+  TORCH_CHECK(b.scalar_type() == a.scalar_type(), "gemm_nt_w4: A / B dtype mismatch");
   FT_CHECK_CONTIG(a);
   FT_CHECK_CONTIG(b);
   TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && a.size(1) == b.size(1), "gemm_nt_w4: A [M, K], B [N, K]");
@@ -418,7 +434,7 @@ at::Tensor gemm_nt_w4(const at::Tensor& a, const at::Tensor& b, const std::optio
   at::Tensor c;
   if (out.has_value() && out->defined()) {
     c = *out;
-    FT_CHECK_BF16(c);
+    TORCH_CHECK(c.scalar_type() == a.scalar_type(), "gemm_nt_w4: out dtype");
     FT_CHECK_CONTIG(c);
     TORCH_CHECK(c.numel() == M * N, "gemm_nt_w4: out has the wrong size");
   } else {
@@ -439,18 +455,13 @@ at::Tensor gemm_nt_w4(const at::Tensor& a, const at::Tensor& b, const std::optio
   p.tiles_n = N / (32 * NJ);
   int epi = W4_STORE;
   if (residual.has_value() && residual->defined()) {
-    FT_CHECK_BF16((*residual));
+    TORCH_CHECK(residual->scalar_type() == a.scalar_type(), "gemm_nt_w4: residual dtype");
     FT_CHECK_CONTIG((*residual));
     TORCH_CHECK(residual->numel() == M * N, "gemm_nt_w4: residual has the wrong size");
     p.r = cptr<bf16_t>(*residual);
     epi = W4_RES;
   }
-  switch (NJ) {
-    case 8: launch_nj<8>(p, epi, ft_stream()); break;
-    case 7: launch_nj<7>(p, epi, ft_stream()); break;
-    case 6: launch_nj<6>(p, epi, ft_stream()); break;
-    default: launch_nj<4>(p, epi, ft_stream()); break;
-  }
+  launch(a.scalar_type(), NJ, p, epi, ft_stream());
   FT_LAUNCH_CHECK();
   return c;
 }
@@ -460,8 +471,8 @@ at::Tensor gemm_nt_w4(const at::Tensor& a, const at::Tensor& b, const std::optio
 at::Tensor gemm_qkv_rope_w4(const at::Tensor& x, const at::Tensor& w, const at::Tensor& cos_t,
                             const at::Tensor& sin_t, int64_t seq, int64_t hq, int64_t hkv, int64_t d) {
   FT_CHECK_CUDA(x);
-  FT_CHECK_BF16(x);
-  FT_CHECK_BF16(w);
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kHalf, "gemm_qkv_rope_w4: bf16 / fp16");
+  TORCH_CHECK(w.scalar_type() == x.scalar_type(), "gemm_qkv_rope_w4: x / w dtype mismatch");
   FT_CHECK_CONTIG(x);
   FT_CHECK_CONTIG(w);
   FT_CHECK_F32(cos_t);
@@ -493,12 +504,7 @@ at::Tensor gemm_qkv_rope_w4(const at::Tensor& x, const at::Tensor& w, const at::
   p.rope_cols = (int)((hq + hkv) * d);
   p.rope_hd = (int)d;
   p.rope_seq = (int)seq;
-  switch (NJ) {
-    case 8: launch_nj<8>(p, W4_ROPE, ft_stream()); break;
-    case 7: launch_nj<7>(p, W4_ROPE, ft_stream()); break;
-    case 6: launch_nj<6>(p, W4_ROPE, ft_stream()); break;
-    default: launch_nj<4>(p, W4_ROPE, ft_stream()); break;
-  }
+  launch(x.scalar_type(), NJ, p, W4_ROPE, ft_stream());
   FT_LAUNCH_CHECK();
   return c;
 }

@@ -6,12 +6,12 @@
 // `norm_type="layernorm"` (reference model.py:19, declared but unused there)
 // selects the mean-subtracting variant.
 //
-// Layout: one wave (64 lanes) per row, 8 contiguous bf16 (one 16-B load) per
-// lane per 512-column chunk; the whole row stays in VGPRs between the reduction
-// and the write (one HBM read + one write per element). Backward writes
-// per-wave fp32 dW partials (no atomics → deterministic) that a column-parallel
-// kernel folds into the bf16 weight gradient, which is written straight into
-// the flat gradient buffer. Backward grid: ~2 rows per wave so every CU gets
+// Layout: one wave (64 lanes) per row, 8 contiguous elements (one 16-B load for
+// bf16 / fp16, 32 B for fp32 under --model-dtype) per lane per 512-column chunk;
+// the whole row stays in VGPRs between the reduction and the write (one HBM read
+// + one write per element). Backward writes per-wave fp32 dW partials (no atomics
+// → deterministic) that a column-parallel kernel folds into the weight gradient,
+// which is written straight into the flat gradient buffer. Backward grid: ~2 rows per wave so every CU gets
 // work (rows are independent; a 64-block grid left 3/4 of the chip idle).
 #include "torch_utils.h"
 
@@ -20,37 +20,37 @@ namespace {
 constexpr int ROWS_PER_BLOCK = 4;  // 4 waves x 64 lanes
 
 // With ADD: the residual add of the previous sub-block is fused in —
-// h1 = bf16(x + d) is written to `hout` (the residual stream) and normalised, so
+// h1 = x + d (rounded to the model dtype) is written to `hout` (the residual stream) and normalised, so
 // the projection GEMMs never need a C input (hipBLASLt copies C into a fresh
 // output first) and h1 is read once. Same rounding as the unfused
-// `x = x + f(x)` (bf16 add) followed by the norm.
-template <int CH, bool LN, bool ADD>
-__global__ __launch_bounds__(256) void norm_fwd_kernel(const bf16_t* __restrict__ x,
-                                                       const bf16_t* __restrict__ d,
-                                                       bf16_t* __restrict__ hout,
-                                                       const bf16_t* __restrict__ w,
-                                                       bf16_t* __restrict__ y,
+// `x = x + f(x)` (model-dtype add) followed by the norm.
+template <class E, int CH, bool LN, bool ADD>
+__global__ __launch_bounds__(256) void norm_fwd_kernel(const typename E::T* __restrict__ x,
+                                                       const typename E::T* __restrict__ d,
+                                                       typename E::T* __restrict__ hout,
+                                                       const typename E::T* __restrict__ w,
+                                                       typename E::T* __restrict__ y,
                                                        float* __restrict__ rstd,
                                                        float* __restrict__ mean_out, int M,
                                                        int N, float eps) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * ROWS_PER_BLOCK + (threadIdx.x >> 6);
   if (row >= M) return;
-  const bf16_t* xr = x + (size_t)row * N;
+  using T = typename E::T;
+  const T* xr = x + (size_t)row * N;
   float v[CH][8];
   float s = 0.f;
 #pragma unroll
   for (int c = 0; c < CH; ++c) {
     const int idx = c * 512 + lane * 8;
     if (idx < N) {
-      uint4 raw = *reinterpret_cast<const uint4*>(xr + idx);
-      unpack8(raw, v[c]);
+      ld8<E>(xr + idx, v[c]);
       if constexpr (ADD) {
         float dv[8];
-        unpack8(*reinterpret_cast<const uint4*>(d + (size_t)row * N + idx), dv);
+        ld8<E>(d + (size_t)row * N + idx, dv);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[c][j] = bf2f(f2bf(v[c][j] + dv[j]));
-        *reinterpret_cast<uint4*>(hout + (size_t)row * N + idx) = pack8(v[c]);
+        for (int j = 0; j < 8; ++j) v[c][j] = rnd<E>(v[c][j] + dv[j]);
+        st8<E>(hout + (size_t)row * N + idx, v[c]);
       }
     } else {
 #pragma unroll
@@ -77,16 +77,16 @@ __global__ __launch_bounds__(256) void norm_fwd_kernel(const bf16_t* __restrict_
   }
   ss = wave_sum(ss);
   const float r = rsqrtf(ss / (float)N + eps);
-  bf16_t* yr = y + (size_t)row * N;
+  T* yr = y + (size_t)row * N;
 #pragma unroll
   for (int c = 0; c < CH; ++c) {
     const int idx = c * 512 + lane * 8;
     if (idx < N) {
       float wf[8], o[8];
-      unpack8(*reinterpret_cast<const uint4*>(w + idx), wf);
+      ld8<E>(w + idx, wf);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = bf2f(f2bf((v[c][j] - mu) * r)) * wf[j];
-      *reinterpret_cast<uint4*>(yr + idx) = pack8(o);
+      for (int j = 0; j < 8; ++j) o[j] = rnd<E>((v[c][j] - mu) * r) * wf[j];
+      st8<E>(yr + idx, o);
     }
   }
   if (lane == 0) {
@@ -97,23 +97,25 @@ __global__ __launch_bounds__(256) void norm_fwd_kernel(const bf16_t* __restrict_
 
 // dx = r * (dn - mean(dn) [LN only] - n * mean(dn * n)),  dn = dy * w, n = (x - mu) * r
 // dw_partial[wave_slot][col] += dy * n
-template <int CH, bool LN>
+template <class E, int CH, bool LN>
 __global__ __launch_bounds__(256) void norm_bwd_kernel(
-    const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
-    const float* __restrict__ rstd, const float* __restrict__ mean_in, bf16_t* __restrict__ dx,
-    const bf16_t* __restrict__ dres, float* __restrict__ dw_part, int M, int N) {
-  // Row data is kept packed (bf16) in VGPRs; fp32 values are recomputed per pass
+    const typename E::T* __restrict__ dy, const typename E::T* __restrict__ x,
+    const typename E::T* __restrict__ w, const float* __restrict__ rstd,
+    const float* __restrict__ mean_in, typename E::T* __restrict__ dx,
+    const typename E::T* __restrict__ dres, float* __restrict__ dw_part, int M, int N) {
+  using T = typename E::T;
+  // Row data is kept packed (model dtype) in VGPRs; fp32 values are recomputed per pass
   // to keep the register footprint at ~3 x CH x 4 + 8 x CH VGPRs.
   const int lane = threadIdx.x & 63;
   const int slot = blockIdx.x * ROWS_PER_BLOCK + (threadIdx.x >> 6);
   const int nslots = gridDim.x * ROWS_PER_BLOCK;
-  uint4 wr[CH];  // (N <= 8192: the LDS fold below needs N*4 bytes)
+  P8<E> wr[CH];  // (N <= 8192: the LDS fold below needs N*4 bytes)
   float acc[CH][8];
-  const uint4 z = make_uint4(0, 0, 0, 0);
+  const P8<E> z = zp8<E>();
 #pragma unroll
   for (int c = 0; c < CH; ++c) {
     const int idx = c * 512 + lane * 8;
-    wr[c] = idx < N ? *reinterpret_cast<const uint4*>(w + idx) : z;
+    wr[c] = idx < N ? ldp8<E>(w + idx) : z;
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[c][j] = 0.f;
   }
@@ -121,25 +123,25 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(
   for (int row = slot; row < M; row += nslots) {
     const float r = rstd[row];
     const float mu = LN ? mean_in[row] : 0.f;
-    const bf16_t* xr = x + (size_t)row * N;
-    const bf16_t* dyr = dy + (size_t)row * N;
-    const bf16_t* drr = dres ? dres + (size_t)row * N : nullptr;
+    const T* xr = x + (size_t)row * N;
+    const T* dyr = dy + (size_t)row * N;
+    const T* drr = dres ? dres + (size_t)row * N : nullptr;
     // all three row loads are issued together (one HBM round trip per row, not two)
-    uint4 xv[CH], gv[CH], rv[CH];
+    P8<E> xv[CH], gv[CH], rv[CH];
 #pragma unroll
     for (int c = 0; c < CH; ++c) {
       const int idx = c * 512 + lane * 8;
-      xv[c] = idx < N ? *reinterpret_cast<const uint4*>(xr + idx) : z;
-      gv[c] = idx < N ? *reinterpret_cast<const uint4*>(dyr + idx) : z;
-      rv[c] = (drr && idx < N) ? *reinterpret_cast<const uint4*>(drr + idx) : z;
+      xv[c] = idx < N ? ldp8<E>(xr + idx) : z;
+      gv[c] = idx < N ? ldp8<E>(dyr + idx) : z;
+      rv[c] = (drr && idx < N) ? ldp8<E>(drr + idx) : z;
     }
     float sdn = 0.f, sdnn = 0.f;
 #pragma unroll
     for (int c = 0; c < CH; ++c) {
       float xf[8], g[8], wf[8];
-      unpack8(xv[c], xf);
-      unpack8(gv[c], g);
-      unpack8(wr[c], wf);
+      unp8<E>(xv[c], xf);
+      unp8<E>(gv[c], g);
+      unp8<E>(wr[c], wf);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float n = (xf[j] - mu) * r;
@@ -151,15 +153,15 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(
     }
     sdnn = wave_sum(sdnn) * invN;
     if (LN) sdn = wave_sum(sdn) * invN;
-    bf16_t* dxr = dx + (size_t)row * N;
+    T* dxr = dx + (size_t)row * N;
 #pragma unroll
     for (int c = 0; c < CH; ++c) {
       const int idx = c * 512 + lane * 8;
       if (idx < N) {
         float xf[8], g[8], wf[8], o[8];
-        unpack8(xv[c], xf);
-        unpack8(gv[c], g);
-        unpack8(wr[c], wf);
+        unp8<E>(xv[c], xf);
+        unp8<E>(gv[c], g);
+        unp8<E>(wr[c], wf);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const float n = (xf[j] - mu) * r;
@@ -167,11 +169,11 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(
         }
         if (drr) {
           float rr[8];
-          unpack8(rv[c], rr);
+          unp8<E>(rv[c], rr);
 #pragma unroll
           for (int j = 0; j < 8; ++j) o[j] += rr[j];
         }
-        *reinterpret_cast<uint4*>(dxr + idx) = pack8(o);
+        st8<E>(dxr + idx, o);
       }
     }
   }
@@ -219,25 +221,27 @@ constexpr int SPLIT = 4;    // waves per row
 constexpr int GROUPS = 4;   // row groups per block
 constexpr int RPI = 1;      // rows per group per iteration (loads issued together)
 
-template <int CHW, bool LN>
+template <class E, int CHW, bool LN>
 __global__ __launch_bounds__(1024) void norm_bwd_split_kernel(
-    const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
-    const float* __restrict__ rstd, const float* __restrict__ mean_in, bf16_t* __restrict__ dx,
-    const bf16_t* __restrict__ dres, float* __restrict__ dw_part, int M, int N,
+    const typename E::T* __restrict__ dy, const typename E::T* __restrict__ x,
+    const typename E::T* __restrict__ w, const float* __restrict__ rstd,
+    const float* __restrict__ mean_in, typename E::T* __restrict__ dx,
+    const typename E::T* __restrict__ dres, float* __restrict__ dw_part, int M, int N,
     int rows_per_block) {
+  using T = typename E::T;
   __shared__ float sums[2][GROUPS][RPI][2][SPLIT];  // [parity][group][row][sdnn|sdn][wave]
   extern __shared__ __attribute__((aligned(16))) float red[];  // [N]
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int q = wave % SPLIT, grp = wave / SPLIT;
   const int row0 = blockIdx.x * rows_per_block;
-  const uint4 z = make_uint4(0, 0, 0, 0);
-  uint4 wr[CHW];
+  const P8<E> z = zp8<E>();
+  P8<E> wr[CHW];
   float acc[CHW][8];
 #pragma unroll
   for (int c = 0; c < CHW; ++c) {
     const int idx = (c * SPLIT + q) * 512 + lane * 8;
-    wr[c] = idx < N ? *reinterpret_cast<const uint4*>(w + idx) : z;
+    wr[c] = idx < N ? ldp8<E>(w + idx) : z;
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[c][j] = 0.f;
   }
@@ -246,7 +250,7 @@ __global__ __launch_bounds__(1024) void norm_bwd_split_kernel(
   for (int it = 0; it < iters; ++it) {
     const int par = it & 1;
     int rows[RPI];
-    uint4 xv[RPI][CHW], gv[RPI][CHW];
+    P8<E> xv[RPI][CHW], gv[RPI][CHW];
 #pragma unroll
     for (int k = 0; k < RPI; ++k) {
       const int rr = row0 + (it * RPI + k) * GROUPS + grp;
@@ -256,8 +260,8 @@ __global__ __launch_bounds__(1024) void norm_bwd_split_kernel(
       for (int c = 0; c < CHW; ++c) {
         const int idx = (c * SPLIT + q) * 512 + lane * 8;
         const bool ok = rows[k] >= 0 && idx < N;
-        xv[k][c] = ok ? *reinterpret_cast<const uint4*>(x + off + idx) : z;
-        gv[k][c] = ok ? *reinterpret_cast<const uint4*>(dy + off + idx) : z;
+        xv[k][c] = ok ? ldp8<E>(x + off + idx) : z;
+        gv[k][c] = ok ? ldp8<E>(dy + off + idx) : z;
       }
     }
     float r[RPI], mu[RPI];
@@ -269,9 +273,9 @@ __global__ __launch_bounds__(1024) void norm_bwd_split_kernel(
 #pragma unroll
       for (int c = 0; c < CHW; ++c) {
         float xf[8], g[8], wf[8];
-        unpack8(xv[k][c], xf);
-        unpack8(gv[k][c], g);
-        unpack8(wr[c], wf);
+        unp8<E>(xv[k][c], xf);
+        unp8<E>(gv[k][c], g);
+        unp8<E>(wr[c], wf);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const float n = (xf[j] - mu[k]) * r[k];
@@ -295,12 +299,11 @@ __global__ __launch_bounds__(1024) void norm_bwd_split_kernel(
     for (int k = 0; k < RPI; ++k)
 #pragma unroll
       for (int c = 0; c < CHW; ++c) {
-        asm volatile("" : "+v"(xv[k][c].x), "+v"(xv[k][c].y), "+v"(xv[k][c].z), "+v"(xv[k][c].w));
-        asm volatile("" : "+v"(gv[k][c].x), "+v"(gv[k][c].y), "+v"(gv[k][c].z), "+v"(gv[k][c].w));
+        pin8<E>(xv[k][c]);
+        pin8<E>(gv[k][c]);
       }
 #pragma unroll
-    for (int c = 0; c < CHW; ++c)
-      asm volatile("" : "+v"(wr[c].x), "+v"(wr[c].y), "+v"(wr[c].z), "+v"(wr[c].w));
+    for (int c = 0; c < CHW; ++c) pin8<E>(wr[c]);
 #pragma unroll
     for (int k = 0; k < RPI; ++k) {
       if (rows[k] < 0) continue;
@@ -312,15 +315,15 @@ __global__ __launch_bounds__(1024) void norm_bwd_split_kernel(
       }
       sdnn *= invN;
       sdn *= invN;
-      bf16_t* dxr = dx + (size_t)rows[k] * N;
+      T* dxr = dx + (size_t)rows[k] * N;
 #pragma unroll
       for (int c = 0; c < CHW; ++c) {
         const int idx = (c * SPLIT + q) * 512 + lane * 8;
         if (idx < N) {
           float xf[8], g[8], wf[8], o[8];
-          unpack8(xv[k][c], xf);
-          unpack8(gv[k][c], g);
-          unpack8(wr[c], wf);
+          unp8<E>(xv[k][c], xf);
+          unp8<E>(gv[k][c], g);
+          unp8<E>(wr[c], wf);
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
             const float n = (xf[j] - mu[k]) * r[k];
@@ -328,11 +331,11 @@ __global__ __launch_bounds__(1024) void norm_bwd_split_kernel(
           }
           if (dres) {  // loaded after the barrier: keeps the pre-barrier set at 2 operands
             float rr[8];
-            unpack8(*reinterpret_cast<const uint4*>(dres + (size_t)rows[k] * N + idx), rr);
+            ld8<E>(dres + (size_t)rows[k] * N + idx, rr);
 #pragma unroll
             for (int j = 0; j < 8; ++j) o[j] += rr[j];
           }
-          *reinterpret_cast<uint4*>(dxr + idx) = pack8(o);
+          st8<E>(dxr + idx, o);
         }
       }
     }
@@ -365,11 +368,12 @@ __global__ __launch_bounds__(1024) void norm_bwd_split_kernel(
     *reinterpret_cast<float4*>(part + i) = *reinterpret_cast<const float4*>(red + i);
 }
 
-// Column sums of a [P, N] fp32 slab -> bf16 dw (optionally accumulated).
+// Column sums of a [P, N] fp32 slab -> model-dtype dw (optionally accumulated).
 // Block = 32 columns x 8 row groups (128-B row segments); fixed summation order
 // (deterministic). 128 blocks for N = 4096.
+template <class E>
 __global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ part,
-                                                     bf16_t* __restrict__ dw, int P, int N,
+                                                     typename E::T* __restrict__ dw, int P, int N,
                                                      bool accumulate) {
   __shared__ float red[8][33];
   const int cl = threadIdx.x & 31, g = threadIdx.x >> 5;
@@ -385,18 +389,19 @@ __global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ p
     float t = 0.f;
 #pragma unroll
     for (int k = 0; k < 8; ++k) t += red[k][cl];
-    if (accumulate) t += bf2f(dw[col]);
-    dw[col] = f2bf(t);
+    if (accumulate) t += ld1<E>(dw + col);
+    dw[col] = cvt1<E>(t);
   }
 }
 
-template <bool LN, bool ADD>
-void launch_fwd(const bf16_t* x, const bf16_t* d, bf16_t* hout, const bf16_t* w, bf16_t* y,
-                float* rstd, float* mean, int M, int N, float eps, hipStream_t st) {
+template <class E, bool LN, bool ADD>
+void launch_fwd(const typename E::T* x, const typename E::T* d, typename E::T* hout,
+                const typename E::T* w, typename E::T* y, float* rstd, float* mean, int M, int N,
+                float eps, hipStream_t st) {
   const int chunks = (N + 511) / 512;
   dim3 grid((M + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK), block(256);
 #define FT_NF(C)                                                                             \
-  hipLaunchKernelGGL((norm_fwd_kernel<C, LN, ADD>), grid, block, 0, st, x, d, hout, w, y, rstd, \
+  hipLaunchKernelGGL((norm_fwd_kernel<E, C, LN, ADD>), grid, block, 0, st, x, d, hout, w, y, rstd, \
                      mean, M, N, eps)
   if (chunks <= 1) FT_NF(1);
   else if (chunks <= 2) FT_NF(2);
@@ -425,15 +430,16 @@ void split_grid(int M, int* nblk, int* rows_per_block) {
   *nblk = std::max(1, (M + rpb - 1) / rpb);
 }
 
-template <bool LN>
-void launch_bwd_split(const bf16_t* dy, const bf16_t* x, const bf16_t* w, const float* rstd,
-                      const float* mean, bf16_t* dx, const bf16_t* dres, float* part, int nblk,
-                      int rows_per_block, int M, int N, hipStream_t st) {
+template <class E, bool LN>
+void launch_bwd_split(const typename E::T* dy, const typename E::T* x, const typename E::T* w,
+                      const float* rstd, const float* mean, typename E::T* dx,
+                      const typename E::T* dres, float* part, int nblk, int rows_per_block, int M,
+                      int N, hipStream_t st) {
   const int chw = ((N + 511) / 512 + SPLIT - 1) / SPLIT;
   dim3 grid(nblk), block(1024);
   const size_t lds = (size_t)N * sizeof(float);
 #define FT_NBS(C)                                                                       \
-  hipLaunchKernelGGL((norm_bwd_split_kernel<C, LN>), grid, block, lds, st, dy, x, w, rstd, \
+  hipLaunchKernelGGL((norm_bwd_split_kernel<E, C, LN>), grid, block, lds, st, dy, x, w, rstd, \
                      mean, dx, dres, part, M, N, rows_per_block)
   if (chw <= 1) FT_NBS(1);
   else if (chw <= 2) FT_NBS(2);
@@ -442,15 +448,15 @@ void launch_bwd_split(const bf16_t* dy, const bf16_t* x, const bf16_t* w, const 
 #undef FT_NBS
 }
 
-template <bool LN>
-void launch_bwd(const bf16_t* dy, const bf16_t* x, const bf16_t* w, const float* rstd,
-                const float* mean, bf16_t* dx, const bf16_t* dres, float* part, int nblk, int M,
-                int N, hipStream_t st) {
+template <class E, bool LN>
+void launch_bwd(const typename E::T* dy, const typename E::T* x, const typename E::T* w,
+                const float* rstd, const float* mean, typename E::T* dx, const typename E::T* dres,
+                float* part, int nblk, int M, int N, hipStream_t st) {
   const int chunks = (N + 511) / 512;
   dim3 grid(nblk), block(256);
   const size_t lds = (size_t)N * sizeof(float);
 #define FT_NB(C)                                                                            \
-  hipLaunchKernelGGL((norm_bwd_kernel<C, LN>), grid, block, lds, st, dy, x, w, rstd, mean, dx, \
+  hipLaunchKernelGGL((norm_bwd_kernel<E, C, LN>), grid, block, lds, st, dy, x, w, rstd, mean, dx, \
                      dres, part, M, N)
   if (chunks <= 1) FT_NB(1);
   else if (chunks <= 2) FT_NB(2);
@@ -464,22 +470,23 @@ void launch_bwd(const bf16_t* dy, const bf16_t* x, const bf16_t* w, const float*
 }  // namespace
 
 // Returns (y, rstd, mean, h). `mean` is empty for RMSNorm. With `d` given, the input
-// is h = bf16(x + d) (fused residual add) and h is returned; otherwise h is empty.
+// is h = x + d rounded to the model dtype (fused residual add) and h is returned;
+// otherwise h is empty. x, d, w, y, h: bf16 / fp16 / fp32 (one dtype).
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> add_norm_fwd(
     const at::Tensor& x, const std::optional<at::Tensor>& d, const at::Tensor& w, double eps,
     bool layernorm) {
   FT_CHECK_CUDA(x);
-  FT_CHECK_BF16(x);
-  FT_CHECK_BF16(w);
+  FT_CHECK_MODEL_DTYPE(x);
   FT_CHECK_CONTIG(x);
   FT_CHECK_CONTIG(w);
+  TORCH_CHECK(w.scalar_type() == x.scalar_type(), "norm: weight dtype must match x");
   const int N = x.size(-1);
   TORCH_CHECK(w.numel() == N, "norm: weight size mismatch");
   TORCH_CHECK(N % 8 == 0, "norm: N must be a multiple of 8");
   const int M = x.numel() / N;
   const bool add = d.has_value() && d->defined();
   if (add) {
-    FT_CHECK_BF16((*d));
+    TORCH_CHECK(d->scalar_type() == x.scalar_type(), "add_norm: delta dtype must match x");
     FT_CHECK_CONTIG((*d));
     TORCH_CHECK(d->numel() == x.numel(), "add_norm: residual delta shape mismatch");
   }
@@ -489,13 +496,21 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> add_norm_fwd(
   at::Tensor mean = at::empty({layernorm ? M : 0}, x.options().dtype(at::kFloat));
   at::Tensor h = add ? at::empty_like(x) : at::empty({0}, x.options());
   if (M == 0) return {y, rstd, mean, h};
-  const bf16_t* dp = add ? cptr<bf16_t>(*d) : nullptr;
-  bf16_t* hp = add ? mptr<bf16_t>(h) : nullptr;
   float* mp = layernorm ? mptr<float>(mean) : nullptr;
-  if (layernorm && add) launch_fwd<true, true>(cptr<bf16_t>(x), dp, hp, cptr<bf16_t>(w), mptr<bf16_t>(y), mptr<float>(rstd), mp, M, N, (float)eps, ft_stream());
-  else if (layernorm) launch_fwd<true, false>(cptr<bf16_t>(x), dp, hp, cptr<bf16_t>(w), mptr<bf16_t>(y), mptr<float>(rstd), mp, M, N, (float)eps, ft_stream());
-  else if (add) launch_fwd<false, true>(cptr<bf16_t>(x), dp, hp, cptr<bf16_t>(w), mptr<bf16_t>(y), mptr<float>(rstd), mp, M, N, (float)eps, ft_stream());
-  else launch_fwd<false, false>(cptr<bf16_t>(x), dp, hp, cptr<bf16_t>(w), mptr<bf16_t>(y), mptr<float>(rstd), mp, M, N, (float)eps, ft_stream());
+  FT_DISPATCH_E(x.scalar_type(), {
+    using T = typename E::T;
+    const T* dp = add ? cptr<T>(*d) : nullptr;
+    T* hp = add ? mptr<T>(h) : nullptr;
+    auto go = [&](auto ln, auto ad) {
+      launch_fwd<E, decltype(ln)::value, decltype(ad)::value>(
+          cptr<T>(x), dp, hp, cptr<T>(w), mptr<T>(y), mptr<float>(rstd), mp, M, N, (float)eps,
+          ft_stream());
+    };
+    if (layernorm && add) go(std::true_type{}, std::true_type{});
+    else if (layernorm) go(std::true_type{}, std::false_type{});
+    else if (add) go(std::false_type{}, std::true_type{});
+    else go(std::false_type{}, std::false_type{});
+  });
   FT_LAUNCH_CHECK();
   return {y, rstd, mean, h};
 }
@@ -517,13 +532,13 @@ std::tuple<at::Tensor, at::Tensor> norm_bwd_part(const at::Tensor& dy, const at:
                                                  const std::optional<at::Tensor>& mean,
                                                  const std::optional<at::Tensor>& dres) {
   FT_CHECK_CUDA(dy);
-  FT_CHECK_BF16(dy);
   FT_CHECK_CONTIG(dy);
   FT_CHECK_CUDA(x);
-  FT_CHECK_BF16(x);
+  FT_CHECK_MODEL_DTYPE(x);
   FT_CHECK_CONTIG(x);
-  FT_CHECK_BF16(w);
   FT_CHECK_CONTIG(w);
+  TORCH_CHECK(dy.scalar_type() == x.scalar_type() && w.scalar_type() == x.scalar_type(),
+              "norm_bwd: dy, x and w must share one dtype");
   FT_CHECK_F32(rstd);
   FT_CHECK_CONTIG(rstd);
   const int N = x.size(-1);
@@ -534,12 +549,11 @@ std::tuple<at::Tensor, at::Tensor> norm_bwd_part(const at::Tensor& dy, const at:
   const at::DeviceGuard guard(x.device());
   auto dx = at::empty_like(x);
   const bool ln = mean.has_value() && mean->defined() && mean->numel() > 0;
-  const bf16_t* dr = nullptr;
-  if (dres.has_value() && dres->defined()) {
-    FT_CHECK_BF16((*dres));
+  const bool has_dres = dres.has_value() && dres->defined();
+  if (has_dres) {
+    TORCH_CHECK(dres->scalar_type() == x.scalar_type(), "norm_bwd: dres dtype must match x");
     FT_CHECK_CONTIG((*dres));
     TORCH_CHECK(dres->numel() == x.numel(), "norm_bwd: dres shape mismatch");
-    dr = cptr<bf16_t>(*dres);
   }
   // ~2 rows per wave: enough blocks to cover all 256 CUs, few enough partial rows
   int nblk = std::max(1, std::min((M + ROWS_PER_BLOCK * 2 - 1) / (ROWS_PER_BLOCK * 2), 256));
@@ -547,42 +561,48 @@ std::tuple<at::Tensor, at::Tensor> norm_bwd_part(const at::Tensor& dy, const at:
   int rows_per_block = 0;
   if (split) split_grid(M, &nblk, &rows_per_block);
   auto part = at::empty({(long)nblk, N}, x.options().dtype(at::kFloat));
-  if (split) {
-    if (ln)
-      launch_bwd_split<true>(cptr<bf16_t>(dy), cptr<bf16_t>(x), cptr<bf16_t>(w), cptr<float>(rstd),
-                             cptr<float>(*mean), mptr<bf16_t>(dx), dr, mptr<float>(part), nblk,
-                             rows_per_block, M, N, ft_stream());
-    else
-      launch_bwd_split<false>(cptr<bf16_t>(dy), cptr<bf16_t>(x), cptr<bf16_t>(w), cptr<float>(rstd),
-                              nullptr, mptr<bf16_t>(dx), dr, mptr<float>(part), nblk,
-                              rows_per_block, M, N, ft_stream());
-    FT_LAUNCH_CHECK();
-  } else if (M > 0) {
-    if (ln)
-      launch_bwd<true>(cptr<bf16_t>(dy), cptr<bf16_t>(x), cptr<bf16_t>(w), cptr<float>(rstd),
-                       cptr<float>(*mean), mptr<bf16_t>(dx), dr, mptr<float>(part), nblk, M, N,
-                       ft_stream());
-    else
-      launch_bwd<false>(cptr<bf16_t>(dy), cptr<bf16_t>(x), cptr<bf16_t>(w), cptr<float>(rstd),
-                        nullptr, mptr<bf16_t>(dx), dr, mptr<float>(part), nblk, M, N,
-                        ft_stream());
+  const float* mp = ln ? cptr<float>(*mean) : nullptr;
+  if (M > 0) {
+    FT_DISPATCH_E(x.scalar_type(), {
+      using T = typename E::T;
+      const T* dr = has_dres ? cptr<T>(*dres) : nullptr;
+      if (split) {
+        if (ln)
+          launch_bwd_split<E, true>(cptr<T>(dy), cptr<T>(x), cptr<T>(w), cptr<float>(rstd), mp,
+                                    mptr<T>(dx), dr, mptr<float>(part), nblk, rows_per_block, M,
+                                    N, ft_stream());
+        else
+          launch_bwd_split<E, false>(cptr<T>(dy), cptr<T>(x), cptr<T>(w), cptr<float>(rstd),
+                                     nullptr, mptr<T>(dx), dr, mptr<float>(part), nblk,
+                                     rows_per_block, M, N, ft_stream());
+      } else {
+        if (ln)
+          launch_bwd<E, true>(cptr<T>(dy), cptr<T>(x), cptr<T>(w), cptr<float>(rstd), mp,
+                              mptr<T>(dx), dr, mptr<float>(part), nblk, M, N, ft_stream());
+        else
+          launch_bwd<E, false>(cptr<T>(dy), cptr<T>(x), cptr<T>(w), cptr<float>(rstd), nullptr,
+                               mptr<T>(dx), dr, mptr<float>(part), nblk, M, N, ft_stream());
+      }
+    });
     FT_LAUNCH_CHECK();
   }
   return {dx, M > 0 ? part : part.narrow(0, 0, 0)};
 }
 
-// dw (bf16, [N]) = column sums of part [P, N] (+ dw when accumulating); fixed order.
+// dw ([N], model dtype) = column sums of part [P, N] (+ dw when accumulating); fixed order.
 void colsum_(const at::Tensor& part, const at::Tensor& dw, bool accumulate) {
   FT_CHECK_CUDA(part);
   FT_CHECK_CONTIG(part);
-  FT_CHECK_BF16(dw);
+  FT_CHECK_MODEL_DTYPE(dw);
   FT_CHECK_CONTIG(dw);
   TORCH_CHECK(part.scalar_type() == at::kFloat && part.dim() == 2 && part.size(1) == dw.numel(),
               "colsum_: part must be fp32 [P, N] with N = dw.numel()");
   const at::DeviceGuard guard(dw.device());
   const int N = dw.numel();
-  hipLaunchKernelGGL(colsum_kernel, dim3((N + 31) / 32), dim3(256), 0, ft_stream(),
-                     cptr<float>(part), mptr<bf16_t>(dw), (int)part.size(0), N, accumulate);
+  FT_DISPATCH_E(dw.scalar_type(),
+                hipLaunchKernelGGL((colsum_kernel<E>), dim3((N + 31) / 32), dim3(256), 0,
+                                   ft_stream(), cptr<float>(part), mptr<typename E::T>(dw),
+                                   (int)part.size(0), N, accumulate));
   FT_LAUNCH_CHECK();
 }
 

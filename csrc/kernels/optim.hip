@@ -9,7 +9,8 @@
 //  * AdamW: torch.optim.AdamW defaults used by the reference (train.py:68):
 //    betas (0.9, 0.999), eps 1e-8, decoupled weight decay 0.01, bias correction.
 //    Math in fp32, storage in the parameter/state dtype (bf16 by default like
-//    the reference's all-bf16 states). A non-finite norm skips the update for
+//    the reference's all-bf16 states; fp16 / fp32 under --model-dtype, moments
+//    optionally fp32). A non-finite norm skips the update for
 //    every element (the host raises the reference's error path afterwards).
 //
 // The whole model's parameters, gradients and both moments each live in ONE
@@ -45,23 +46,19 @@ __device__ __forceinline__ void st16(void* p, uint4 v) {
   }
 }
 
-template <typename T, bool NT = false>
-struct V8;
-template <bool NT>
-struct V8<bf16_t, NT> {
-  __device__ static void load(const bf16_t* p, float* f) { unpack8(ld16<NT>(p), f); }
-  __device__ static void store(bf16_t* p, const float* f) { st16<NT>(p, pack8(f)); }
-};
-template <bool NT>
-struct V8<float, NT> {
-  __device__ static void load(const float* p, float* f) {
-    const uint4 a = ld16<NT>(p), b = ld16<NT>(p + 4);
-    f[0] = __uint_as_float(a.x); f[1] = __uint_as_float(a.y); f[2] = __uint_as_float(a.z); f[3] = __uint_as_float(a.w);
-    f[4] = __uint_as_float(b.x); f[5] = __uint_as_float(b.y); f[6] = __uint_as_float(b.z); f[7] = __uint_as_float(b.w);
+// 8 elements of element type E (common.h) through 16-B (non-temporal) accesses.
+template <class E, bool NT>
+struct V8 {
+  __device__ static void load(const typename E::T* p, float* f) {
+    P8<E> r;
+    r.v[0] = ld16<NT>(p);
+    if constexpr (!E::is16) r.v[1] = ld16<NT>(p + 4);
+    unp8<E>(r, f);
   }
-  __device__ static void store(float* p, const float* f) {
-    st16<NT>(p, make_uint4(__float_as_uint(f[0]), __float_as_uint(f[1]), __float_as_uint(f[2]), __float_as_uint(f[3])));
-    st16<NT>(p + 4, make_uint4(__float_as_uint(f[4]), __float_as_uint(f[5]), __float_as_uint(f[6]), __float_as_uint(f[7])));
+  __device__ static void store(typename E::T* p, const float* f) {
+    const P8<E> r = pk8<E>(f);
+    st16<NT>(p, r.v[0]);
+    if constexpr (!E::is16) st16<NT>(p + 4, r.v[1]);
   }
 };
 
@@ -76,8 +73,8 @@ bool stream_nt() {
 
 constexpr int NORM_BLOCKS = 2048;
 
-template <typename G, bool NT>
-__global__ __launch_bounds__(256) void sumsq_kernel(const G* __restrict__ g, long n8,
+template <class G, bool NT>
+__global__ __launch_bounds__(256) void sumsq_kernel(const typename G::T* __restrict__ g, long n8,
                                                     float* __restrict__ partial) {
   float s = 0.f;
   for (long i = blockIdx.x * 256L + threadIdx.x; i < n8; i += (long)gridDim.x * 256) {
@@ -126,9 +123,11 @@ __global__ __launch_bounds__(1024) void norm_finish_kernel(const float* __restri
   }
 }
 
-template <typename P, typename S, bool NT>
-__global__ __launch_bounds__(256) void adamw_kernel(P* __restrict__ p, const P* __restrict__ g,
-                                                    S* __restrict__ m, S* __restrict__ v,
+template <class P, class S, bool NT>
+__global__ __launch_bounds__(256) void adamw_kernel(typename P::T* __restrict__ p,
+                                                    const typename P::T* __restrict__ g,
+                                                    typename S::T* __restrict__ m,
+                                                    typename S::T* __restrict__ v,
                                                     long n8, float lr, float beta1, float beta2,
                                                     float eps, float wd, float inv_bc1,
                                                     float inv_sqrt_bc2,
@@ -177,16 +176,14 @@ int stream_grid(long n8) {
 
 void launch_sumsq(const at::Tensor& grad, long n8, int nb, float* partial) {
   const bool nt = stream_nt();
-#define FT_SSQ(G, NT_) \
-  hipLaunchKernelGGL((sumsq_kernel<G, NT_>), dim3(nb), dim3(256), 0, ft_stream(), cptr<G>(grad), n8, partial)
-  if (grad.scalar_type() == at::kBFloat16) {
-    if (nt) FT_SSQ(bf16_t, true); else FT_SSQ(bf16_t, false);
-  } else if (grad.scalar_type() == at::kFloat) {
-    if (nt) FT_SSQ(float, true); else FT_SSQ(float, false);
-  } else {
-    TORCH_CHECK(false, "sumsq: unsupported dtype");
-  }
-#undef FT_SSQ
+  FT_DISPATCH_E(grad.scalar_type(), {
+    if (nt)
+      hipLaunchKernelGGL((sumsq_kernel<E, true>), dim3(nb), dim3(256), 0, ft_stream(),
+                         cptr<typename E::T>(grad), n8, partial);
+    else
+      hipLaunchKernelGGL((sumsq_kernel<E, false>), dim3(nb), dim3(256), 0, ft_stream(),
+                         cptr<typename E::T>(grad), n8, partial);
+  });
 }
 
 }  // namespace
@@ -240,22 +237,29 @@ void adamw_(const at::Tensor& p, const at::Tensor& g, const at::Tensor& m, const
   if (max_blocks > 0) nb = (int)std::max(1L, std::min((n8 + 255) / 256, (long)max_blocks));
   const dim3 grid(nb), block(256);
   const bool nt = stream_nt();
-#define FT_ADAM(PT, ST)                                                                             \
-  do {                                                                                              \
-  if (nt)                                                                                           \
-    hipLaunchKernelGGL((adamw_kernel<PT, ST, true>), grid, block, 0, ft_stream(), mptr<PT>(p),       \
-                       cptr<PT>(g), mptr<ST>(m), mptr<ST>(v), n8, (float)lr, (float)beta1,          \
-                       (float)beta2, (float)eps, (float)wd, inv_bc1, inv_sqrt_bc2, cptr<float>(stats), hp); \
-  else                                                                                              \
-    hipLaunchKernelGGL((adamw_kernel<PT, ST, false>), grid, block, 0, ft_stream(), mptr<PT>(p),      \
-                       cptr<PT>(g), mptr<ST>(m), mptr<ST>(v), n8, (float)lr, (float)beta1,          \
-                       (float)beta2, (float)eps, (float)wd, inv_bc1, inv_sqrt_bc2, cptr<float>(stats), hp); \
-  } while (0)
-  if (p.scalar_type() == at::kBFloat16 && m.scalar_type() == at::kBFloat16) FT_ADAM(bf16_t, bf16_t);
-  else if (p.scalar_type() == at::kBFloat16 && m.scalar_type() == at::kFloat) FT_ADAM(bf16_t, float);
-  else if (p.scalar_type() == at::kFloat && m.scalar_type() == at::kFloat) FT_ADAM(float, float);
-  else TORCH_CHECK(false, "adamw: unsupported dtype combination");
-#undef FT_ADAM
+  // parameter dtype P (= gradient dtype) in {bf16, fp16, fp32}; moments S either P or fp32
+  TORCH_CHECK(m.scalar_type() == p.scalar_type() || m.scalar_type() == at::kFloat,
+              "adamw: optimizer states must have the parameter dtype or fp32");
+  auto go = [&](auto ptag, auto stag) {
+    using P = decltype(ptag);
+    using S = decltype(stag);
+    using PT = typename P::T;
+    using ST = typename S::T;
+    if (nt)
+      hipLaunchKernelGGL((adamw_kernel<P, S, true>), grid, block, 0, ft_stream(), mptr<PT>(p),
+                         cptr<PT>(g), mptr<ST>(m), mptr<ST>(v), n8, (float)lr, (float)beta1,
+                         (float)beta2, (float)eps, (float)wd, inv_bc1, inv_sqrt_bc2,
+                         cptr<float>(stats), hp);
+    else
+      hipLaunchKernelGGL((adamw_kernel<P, S, false>), grid, block, 0, ft_stream(), mptr<PT>(p),
+                         cptr<PT>(g), mptr<ST>(m), mptr<ST>(v), n8, (float)lr, (float)beta1,
+                         (float)beta2, (float)eps, (float)wd, inv_bc1, inv_sqrt_bc2,
+                         cptr<float>(stats), hp);
+  };
+  FT_DISPATCH_E(p.scalar_type(), {
+    if (m.scalar_type() == at::kFloat) go(E{}, EF32{});
+    else go(E{}, E{});
+  });
   FT_LAUNCH_CHECK();
 }
 

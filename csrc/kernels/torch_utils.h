@@ -43,6 +43,21 @@ static inline hipStream_t ft_stream() {
     }                                            \
   } while (0)
 
+// Same for the 16-bit model dtypes only (MFMA kernels: bf16 / fp16).
+#define FT_DISPATCH_E16(ST, ...)                 \
+  do {                                           \
+    const auto _st = (ST);                       \
+    if (_st == at::kBFloat16) {                  \
+      using E = EBF16;                           \
+      __VA_ARGS__;                               \
+    } else if (_st == at::kHalf) {               \
+      using E = EF16;                            \
+      __VA_ARGS__;                               \
+    } else {                                     \
+      TORCH_CHECK(false, "unsupported dtype ", _st, " (bf16 / fp16 only)"); \
+    }                                            \
+  } while (0)
+
 template <typename T>
 static inline const T* cptr(const at::Tensor& t) {
   return reinterpret_cast<const T*>(t.data_ptr());

@@ -10,6 +10,8 @@ from __future__ import annotations
 
 import os
 
+import torch
+
 from .._native import kernels
 
 # Backward variant: 1 = deterministic (default): KV-major dK/dV kernel + Q-major dQ
@@ -25,11 +27,17 @@ def set_deterministic(flag: bool) -> None:
 
 
 def flash_attn_fwd(qk, qkv, S, hq, hkv, d):
-    """Returns (o [T, Hq*D] bf16, lse [B, Hq, S] fp32). The HIP kernel only: no fallback
-    (``kernels()`` raises if the extension is missing)."""
+    """Returns (o [T, Hq*D], lse [B, Hq, S'] fp32) in the model dtype. The HIP kernels only, no
+    fallback (``kernels()`` raises if the extension is missing): the MFMA kernels for bf16 / fp16
+    (csrc/kernels/flash_attn.hip), the fp32 vector-ALU kernels for fp32 models (flash_f32.hip)."""
+    if qk.dtype == torch.float32:
+        return tuple(kernels().flash_f32_fwd(qk, qkv, S, hq, hkv, d))
     return tuple(kernels().flash_fwd(qk, qkv, S, hq, hkv, d))
 
 
 def flash_attn_bwd(do, qk, qkv, o, lse, S, hq, hkv, d):
-    """Returns dqkv [T, (Hq+2Hkv)*D] with dQ/dK still in the rotated frame."""
+    """Returns dqkv [T, (Hq+2Hkv)*D] with dQ/dK still in the rotated frame. Both variants are
+    deterministic (fp32: always; bf16 / fp16: unless FT_FLASH_BWD_MODE=0)."""
+    if qk.dtype == torch.float32:
+        return kernels().flash_f32_bwd(do, qk, qkv, o, lse, S, hq, hkv, d)
     return kernels().flash_bwd(do, qk, qkv, o, lse, S, hq, hkv, d, _BWD_MODE)

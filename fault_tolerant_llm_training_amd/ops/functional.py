@@ -3,6 +3,10 @@
 GPU tensors run the hand-written gfx950 kernels in ``csrc/kernels`` (loaded by
 :func:`fault_tolerant_llm_training_amd._native.kernels`, which raises if the
 library is missing) and hipBLASLt GEMMs through ``torch.mm``/``torch.addmm``.
+Model dtypes (``--model-dtype``): bf16 (every kernel), fp16 (every kernel; the MFMA GEMM and
+flash kernels in their fp16 variants), fp32 (the element-wise / reduction kernels in fp32,
+fp32 attention kernels, fp32 hipBLASLt GEMMs; the bf16-only paths — the round-2 hand GEMM, the
+transpose-based weight gradients, the fused SwiGLU transposes — route by dtype).
 CPU tensors run a pure-PyTorch reference of the same math (the CPU backend for
 the gloo tests); its backward recomputes the forward under autograd.
 
@@ -103,8 +107,11 @@ def set_w4_dw(on: bool) -> None:
     _W4_DW = bool(on)
 
 
+_W4_DTYPES = (torch.bfloat16, torch.float16)  # bf16 / fp16 MFMA variants of the kernel
+
+
 def _w4_fits(x2: torch.Tensor, w: torch.Tensor, max_nj: int = 8) -> bool:
-    if _GEMM_MODE == "blas" or not (x2.is_cuda and x2.dtype == torch.bfloat16 and w.dtype == torch.bfloat16):
+    if _GEMM_MODE == "blas" or not (x2.is_cuda and x2.dtype in _W4_DTYPES and w.dtype == x2.dtype):
         return False
     T, K = x2.shape
     if T % 256 or K % 64:
@@ -606,8 +613,8 @@ def set_qkv_rope(on: bool) -> None:
 
 
 def _qkv_rope_ok(x2: torch.Tensor, w: torch.Tensor, d: int) -> bool:
-    if not (_QKV_ROPE and _GEMM_MODE != "blas" and x2.is_cuda and x2.dtype == torch.bfloat16
-            and w.dtype == torch.bfloat16):
+    if not (_QKV_ROPE and _GEMM_MODE != "blas" and x2.is_cuda and x2.dtype in _W4_DTYPES
+            and w.dtype == x2.dtype):
         return False
     return d % 8 == 0 and _w4_fits(x2, w)
 

@@ -214,8 +214,8 @@ def train(args) -> int:
     monitor = SignalMonitor().install()
     device = info.device
     model_dtype = PRECISION_STR_TO_DTYPE[args.model_dtype]
-    if device.type == "cuda" and model_dtype != torch.bfloat16:
-        raise ValueError("the gfx950 kernels are bf16; use --model-dtype bf16 on the GPU (any dtype on --device cpu)")
+    if device.type == "cuda" and model_dtype not in (torch.bfloat16, torch.float16, torch.float32):
+        raise ValueError("the gfx950 kernels cover --model-dtype bf16, fp16 and fp32 (fp64 on --device cpu only)")
     torch.manual_seed(args.seed)
     from .ops.attention import set_deterministic
 
@@ -267,7 +267,14 @@ def train(args) -> int:
                     "already runs fused gfx950 kernels")
     model.train()
 
-    state_dtype = PRECISION_STR_TO_DTYPE[args.optimizer_state_dtype] if args.optimizer_state_dtype else None
+    # AdamW moments default to the model dtype like the reference, except under fp16: the second
+    # moment g^2 of typical gradients (1e-4 .. 1e-3) is below fp16's normal range, flushes to 0 and
+    # the update m / (sqrt(v) + eps) explodes within a few steps (the tiny preset diverges at step 5
+    # with fp16 moments, on the CPU path too); fp32 moments keep fp16 training stable.
+    if args.optimizer_state_dtype:
+        state_dtype = PRECISION_STR_TO_DTYPE[args.optimizer_state_dtype]
+    else:
+        state_dtype = torch.float32 if model_dtype == torch.float16 else None
     reducer = GradReducer(model.flat, model.sinks_in_backward_order(), bucket_mb=args.dp_bucket_mb,
                           mode=args.dp_mode or None, reduce_dtype=args.dp_reduce_dtype)
     optimizer = FlatAdamW(model.parameters(), model.flat, lr=args.learning_rate, state_dtype=state_dtype,

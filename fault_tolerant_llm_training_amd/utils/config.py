@@ -153,7 +153,7 @@ def build_parser() -> argparse.ArgumentParser:
         "--optimizer-state-dtype",
         type=str,
         default="",
-        help="AdamW moment dtype (bf16/fp32); default = --model-dtype like the reference",
+        help="AdamW moment dtype (bf16/fp16/fp32); default = --model-dtype like the reference (fp32 for fp16 models: fp16 moments underflow)",
     )
     parser.add_argument(
         "--dp-bucket-mb",
