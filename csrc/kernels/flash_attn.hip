@@ -435,6 +435,237 @@ __global__ __launch_bounds__(64 * NW * SPLIT, 8 / (NW * SPLIT)) void flash_fwd_k
   }
 }
 
+// ================================================================== forward, software-pipelined
+// flash_fwd_kernel<E, D, NW, 1> with the scores of key tile j+1 (S^T = K Q^T, 16 MFMAs) issued
+// in the same basic block as tile j's softmax (exp2 / row sum / bf16 packing) and O^T += V^T P^T:
+// the MFMAs of one tile run while the VALU of the previous one issues (intra-wave pipelining, the
+// FA3 "ping-pong inside a warpgroup"), where the unpipelined loop serialises S -> softmax -> PV
+// within the wave and leaves only the co-resident block's wave to fill the gaps.
+// The row max of tile j+1 and the deferred-rescale decision close iteration j (in the shadow of
+// its PV MFMAs), so iteration j+1's exponentials already see the right running max.
+// K and V sit in four LDS objects with different phases: iteration j (phase P = j & 1) reads
+// K(j+1) from kb[P^1] and V(j) from vb[P] while K(j+2) streams into kb[P] and V(j+1) into vb[P^1]
+// (same 64 KiB per block as the unpipelined kernel; no access names a buffer in flight).
+template <class E, int D, int NW = 4>
+__global__ __launch_bounds__(64 * NW, 8 / NW) void flash_fwd_pipe_kernel(
+    const bf16_t* __restrict__ qk, const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out,
+    float* __restrict__ lse2, int B, int S, int Hq, int Hkv, float sl2, long ldqk_) {
+  constexpr int BM = 32 * NW, BN = 64, KS = D / 16, NDB = D / 32;
+  constexpr int TILE = BN * D * 2;
+  __shared__ __attribute__((aligned(16))) char kb0[TILE];
+  __shared__ __attribute__((aligned(16))) char kb1[TILE];
+  __shared__ __attribute__((aligned(16))) char vb0[TILE];
+  __shared__ __attribute__((aligned(16))) char vb1[TILE];
+  typedef typename FA<E>::v8 v8;
+
+  const int nqt = (S + BM - 1) / BM;
+  const int per = B * Hq;
+  const int L = blockIdx.x;
+  int qt;  // heavy / light pairing of the resident blocks, as flash_fwd_kernel
+  if ((nqt & 1) == 0 && L >= (nqt / 2) * per)
+    qt = (L - (nqt / 2) * per) / per;
+  else
+    qt = nqt - 1 - L / per;
+  const int rem = L % per;
+  const int b = rem / Hq;
+  int h, kvh;
+  map_head(rem % Hq, Hq, Hkv, h, kvh);
+
+  const int tid = threadIdx.x, lane = tid & 63, l32 = lane & 31, hi = lane >> 5;
+  const int wave = tid >> 6;
+  const int q0 = qt * BM + wave * 32;
+  const int qrow = q0 + l32;
+  const long ldqk = ldqk_, ldv = (long)(Hq + 2 * Hkv) * D, ldo = (long)Hq * D;
+  const bf16_t* Qg = qk + (long)b * S * ldqk + (long)h * D;
+  const bf16_t* Kg = qk + (long)b * S * ldqk + (long)(Hq + kvh) * D;
+  const bf16_t* Vg = qkv + (long)b * S * ldv + (long)(Hq + Hkv + kvh) * D;
+
+  v8 qf[KS];
+  {
+    const long qr = min(qrow, S - 1);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+      qf[ks] = *reinterpret_cast<const v8*>(Qg + qr * ldqk + ks * 16 + hi * 8);
+  }
+
+  const int kend = min((qt + 1) * BM, S);
+  const int ntiles = (kend + BN - 1) / BN;
+  // the wave's last key tile with an unmasked key (keys <= q0 + 31, < S); < ntiles
+  const int wlast = min(q0 + 31, S - 1) / BN;
+  constexpr int GPW = TILE / 1024 / NW;  // LDS-DMA instructions per wave per image
+  auto dma = [&](const bf16_t* G, long ld, int KT, char* dst) {
+    static_for<GPW>([&](auto I) {
+      const int piece = wave * GPW + I;
+      int r, c;
+      lds_inv<D>(piece * 64 + lane, r, c);
+      const long key = min(KT * BN + r, S - 1);
+      glds16(G + key * ld + c * 8, dst + piece * 1024);
+    });
+  };
+
+  f32x16_t o[NDB];
+#pragma unroll
+  for (int db = 0; db < NDB; ++db)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[db][r] = 0.f;
+  float m = -INFINITY, l = 0.f;
+
+  // S^T of key tile kt (sub-tile 1 skipped when it is wholly above this wave's diagonal)
+  auto scores = [&](const char* kb, int kt, f32x16_t (&s)[2], auto MASKED) {
+    constexpr bool MASK = decltype(MASKED)::value;
+    const bool v1 = kt * BN + 32 <= q0 + 31;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) s[j][r] = 0.f;
+      if (!MASK || j == 0 || v1) {
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) s[j] = mfma32(ld_row<E, D>(kb, j * 32 + l32, 2 * ks + hi), qf[ks], s[j]);
+      }
+    }
+  };
+  // causal mask (diagonal tiles) + row max of the raw scores, both halves of the wave
+  auto rowmax = [&](f32x16_t (&s)[2], int kt, auto MASKED) {
+    constexpr bool MASK = decltype(MASKED)::value;
+    const int k0 = kt * BN;
+    const bool v1 = k0 + 32 <= q0 + 31;
+    float mx = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float x = s[j][r];
+        if constexpr (MASK) {
+          const int key = k0 + j * 32 + (r & 3) + 8 * (r >> 2) + 4 * hi;
+          if ((j == 1 && !v1) || key > qrow) x = -INFINITY;
+          s[j][r] = x;
+        }
+        mx = fmaxf(mx, x);
+      }
+    return max_lane32(mx);
+  };
+  // deferred rescale (see flash_fwd_kernel): decided before the tile's exponentials
+  auto rescale = [&](float mx) {
+    const float cand = mx * sl2;
+    if (__any(cand > m + RESCALE_LOG2)) {
+      const float mn = fmaxf(m, cand);
+      const float alpha = fast_exp2(m - mn);
+      m = mn;
+      l *= alpha;
+#pragma unroll
+      for (int db = 0; db < NDB; ++db)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[db][r] *= alpha;
+    }
+  };
+  // P = exp2(s * c - m) as bf16 fragments, row sum into l
+  auto probs = [&](f32x16_t (&s)[2], v8 (&pb)[4]) {
+    float ls = 0.f;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float p = fast_exp2(fmaf(s[j][r], sl2, -m));
+        ls += p;
+        s[j][r] = p;
+      }
+    pb[0] = cvt8<E, 0>(s[0]);
+    pb[1] = cvt8<E, 8>(s[0]);
+    pb[2] = cvt8<E, 0>(s[1]);
+    pb[3] = cvt8<E, 8>(s[1]);
+    l += ls;
+  };
+  auto pv = [&](const char* vb, const v8 (&pb)[4], bool both) {
+#pragma unroll
+    for (int db = 0; db < NDB; ++db) {
+      o[db] = mfma32(tr_frag<E, D>(vb, 0, db * 32, lane), pb[0], o[db]);
+      o[db] = mfma32(tr_frag<E, D>(vb, 16, db * 32, lane), pb[1], o[db]);
+    }
+    if (both) {
+#pragma unroll
+      for (int db = 0; db < NDB; ++db) {
+        o[db] = mfma32(tr_frag<E, D>(vb, 32, db * 32, lane), pb[2], o[db]);
+        o[db] = mfma32(tr_frag<E, D>(vb, 48, db * 32, lane), pb[3], o[db]);
+      }
+    }
+  };
+
+  // prologue: K(0), V(0), K(1) in flight; tile 0's scores, row max and running max
+  dma(Kg, ldqk, 0, kb0);
+  dma(Vg, ldv, 0, vb0);
+  if (ntiles > 1) dma(Kg, ldqk, 1, kb1);
+  static_for<KS>([&qf](auto I) { asm volatile("" ::"v"(__builtin_bit_cast(u32x4, qf[I]))); });
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  f32x16_t sa[2], sb[2];
+  if (BN - 1 > q0) {
+    scores(kb0, 0, sa, std::true_type{});
+    rescale(rowmax(sa, 0, std::true_type{}));
+  } else {
+    scores(kb0, 0, sa, std::false_type{});
+    rescale(rowmax(sa, 0, std::false_type{}));
+  }
+  __syncthreads();  // K(0) read by every wave before K(2) lands in kb0
+
+  // iteration j, phase P = j & 1: scores of tile j are in (P ? sb : sa), the next tile's go to
+  // the other array (static renaming: the loop is unrolled by two)
+  auto iter = [&](const int j, auto PH) {
+    constexpr int P = decltype(PH)::value;
+    char* kfill = P ? kb1 : kb0;        // K(j) consumed -> K(j + 2)
+    const char* knext = P ? kb0 : kb1;  // K(j + 1)
+    const char* vcur = P ? vb1 : vb0;   // V(j)
+    char* vfill = P ? vb0 : vb1;        // V(j - 1) consumed -> V(j + 1)
+    f32x16_t(&sc)[2] = P ? sb : sa;
+    f32x16_t(&sn)[2] = P ? sa : sb;
+    if (j + 2 < ntiles) dma(Kg, ldqk, j + 2, kfill);
+    if (j + 1 < ntiles) dma(Vg, ldv, j + 1, vfill);
+    if ((j + 2) * BN - 1 <= q0) {
+      // steady state: tiles j and j + 1 wholly below this wave's diagonal — one basic block
+      v8 pb[4];
+      scores(knext, j + 1, sn, std::false_type{});
+      probs(sc, pb);
+      pv(vcur, pb, true);
+      rescale(rowmax(sn, j + 1, std::false_type{}));
+    } else if (j <= wlast) {
+      const bool nxt = j + 1 <= wlast;
+      const bool mask_n = (j + 2) * BN - 1 > q0;
+      if (nxt) {
+        if (mask_n) scores(knext, j + 1, sn, std::true_type{});
+        else scores(knext, j + 1, sn, std::false_type{});
+      }
+      v8 pb[4];
+      probs(sc, pb);
+      pv(vcur, pb, j * BN + 32 <= q0 + 31);
+      if (nxt) {
+        if (mask_n) rescale(rowmax(sn, j + 1, std::true_type{}));
+        else rescale(rowmax(sn, j + 1, std::false_type{}));
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0);  // this wave's DMAs landed ...
+    __syncthreads();                // ... and everyone's; K(j + 1) / V(j) are read
+  };
+  for (int j = 0; j < ntiles; j += 2) {
+    iter(j, std::integral_constant<int, 0>{});
+    if (j + 1 < ntiles) iter(j + 1, std::integral_constant<int, 1>{});
+  }
+
+  l += __shfl_xor(l, 32, 64);
+  const float inv = 1.f / l;
+  if (qrow < S) {
+    bf16_t* orow = out + ((long)b * S + qrow) * ldo + (long)h * D;
+#pragma unroll
+    for (int db = 0; db < NDB; ++db)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        uint2 v;
+        v.x = pk2<E>(o[db][4 * g + 0] * inv, o[db][4 * g + 1] * inv);
+        v.y = pk2<E>(o[db][4 * g + 2] * inv, o[db][4 * g + 3] * inv);
+        *reinterpret_cast<uint2*>(orow + db * 32 + 8 * g + 4 * hi) = v;
+      }
+    if (hi == 0) lse2[((long)b * Hq + h) * stat_stride(S) + qrow] = m + log2f(l);
+  }
+}
+
 // ================================================================== backward
 // delta[b,h,q] = sum_d dO * O   (one 16-lane group per (q, h) row, 8 bf16 per lane step)
 template <class E, int D>
@@ -1156,6 +1387,13 @@ int g_fwd_split = [] {
   return e == nullptr ? -1 : std::atoi(e);
 }();
 
+// Software-pipelined forward (flash_fwd_pipe_kernel) for the unsplit grids: 1 on, 0 off
+// (FT_FLASH_FWD_PIPE / flash_set_fwd_pipe, for A/B).
+int g_fwd_pipe = [] {
+  const char* e = std::getenv("FT_FLASH_FWD_PIPE");
+  return e == nullptr ? 1 : std::atoi(e);
+}();
+
 // dQ key split (see flash_bwd_dq_kernel): -1 default (on), 0 off, 1 on (FT_FLASH_DQ_SPLIT /
 // flash_set_dq_split, for A/B).
 int g_dq_split = [] {
@@ -1237,14 +1475,20 @@ std::tuple<at::Tensor, at::Tensor> flash_fwd(const at::Tensor& qk, const at::Ten
   hipLaunchKernelGGL((flash_fwd_kernel<E, DD, 4, SP>), grid, block, 0, ft_stream(), cptr<bf16_t>(qk), \
                      cptr<bf16_t>(qkv), mptr<bf16_t>(out), mptr<float>(lse), B, (int)S, (int)Hq,   \
                      (int)Hkv, sl2, ldqk)
+#define FT_FWD_PIPE(DD)                                                                            \
+  hipLaunchKernelGGL((flash_fwd_pipe_kernel<E, DD, 4>), grid, block, 0, ft_stream(), cptr<bf16_t>(qk), \
+                     cptr<bf16_t>(qkv), mptr<bf16_t>(out), mptr<float>(lse), B, (int)S, (int)Hq,   \
+                     (int)Hkv, sl2, ldqk)
+  const bool pipe = !split && g_fwd_pipe == 1;
   FT_DISPATCH_E16(qk.scalar_type(), {
     if (D == 128) {
-      if (split) FT_FWD(128, 2); else FT_FWD(128, 1);
+      if (split) FT_FWD(128, 2); else if (pipe) FT_FWD_PIPE(128); else FT_FWD(128, 1);
     } else {
-      if (split) FT_FWD(64, 2); else FT_FWD(64, 1);
+      if (split) FT_FWD(64, 2); else if (pipe) FT_FWD_PIPE(64); else FT_FWD(64, 1);
     }
   });
 #undef FT_FWD
+#undef FT_FWD_PIPE
   FT_LAUNCH_CHECK();
   return {out, lse};
 }
@@ -1364,12 +1608,14 @@ void flash_set_dkdv2(bool on) { g_dkdv2 = on; }
 // Same-process A/B switch of the forward key split: -1 auto, 0 off, 1 on.
 void flash_set_fwd_split(int64_t v) { g_fwd_split = (int)v; }
 void flash_set_dq_split(int64_t v) { g_dq_split = (int)v; }
+void flash_set_fwd_pipe(int64_t v) { g_fwd_pipe = (int)v; }
 void flash_set_kv_split(int64_t v) { g_kv_split = (int)v; }
 
 TORCH_LIBRARY_FRAGMENT(ftamd, m) {
   m.def("flash_set_dkdv2(bool on) -> ()", &flash_set_dkdv2);
   m.def("flash_set_fwd_split(int v) -> ()", &flash_set_fwd_split);
   m.def("flash_set_dq_split(int v) -> ()", &flash_set_dq_split);
+  m.def("flash_set_fwd_pipe(int v) -> ()", &flash_set_fwd_pipe);
   m.def("flash_set_kv_split(int v) -> ()", &flash_set_kv_split);
   m.def("flash_fwd(Tensor qk, Tensor qkv, int S, int Hq, int Hkv, int D) -> (Tensor, Tensor)",
         &flash_fwd);

@@ -135,6 +135,39 @@ def test_flash_fwd_key_split_matches(B, S, Hq, Hkv, D):
     assert rel(g1, g0) < 1e-2
 
 
+@pytest.mark.parametrize("B,S,Hq,Hkv,D", [(1, 2048, 32, 8, 128), (2, 1000, 8, 2, 128), (3, 100, 4, 4, 64),
+                                         (1, 33, 2, 1, 128), (1, 8192, 4, 1, 128), (2, 2047, 8, 8, 64),
+                                         (1, 64, 2, 2, 64), (1, 65, 2, 1, 128)])
+def test_flash_fwd_pipe_matches(B, S, Hq, Hkv, D):
+    """The software-pipelined forward (next tile's scores issued with this tile's softmax) applies
+    the same operations to O / l / m in the same order as the unpipelined kernel: bitwise equal."""
+    from fault_tolerant_llm_training_amd._native import kernels
+
+    K = kernels()
+    torch.manual_seed(5)
+    T = B * S
+    qkv = torch.randn(T, (Hq + 2 * Hkv) * D, device="cuda").bfloat16()
+    qk = torch.randn(T, (Hq + Hkv) * D, device="cuda").bfloat16()
+    try:
+        K.flash_set_fwd_split(0)
+        K.flash_set_fwd_pipe(0)
+        o0, l0 = K.flash_fwd(qk, qkv, S, Hq, Hkv, D)
+        K.flash_set_fwd_pipe(1)
+        o1, l1 = K.flash_fwd(qk, qkv, S, Hq, Hkv, D)
+    finally:
+        K.flash_set_fwd_split(-1)
+        K.flash_set_fwd_pipe(1)
+    valid = torch.arange(l0.shape[-1], device="cuda") < S
+    assert torch.isfinite(o1).all()
+    assert rel(o1, o0) < 1e-3
+    assert (l1[..., valid] - l0[..., valid]).abs().max().item() < 1e-4
+    q = qk[:, : Hq * D].float().view(B, S, Hq, D)
+    k = qk[:, Hq * D :].float().view(B, S, Hkv, D)
+    v = qkv[:, (Hq + Hkv) * D :].float().view(B, S, Hkv, D)
+    if S <= 2048:
+        assert rel(o1.view(B, S, Hq, D), ref_attn(q, k, v)) < 1e-2
+
+
 @pytest.mark.parametrize("B,S,Hq,Hkv,D", [(1, 2048, 12, 12, 64), (2, 320, 8, 2, 128), (1, 100, 4, 4, 64),
                                          (1, 4096, 4, 1, 128)])
 def test_flash_dq_key_split_matches(B, S, Hq, Hkv, D):
