@@ -19,6 +19,21 @@ typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
 typedef float f32x16_t __attribute__((ext_vector_type(16)));
 
+// Hardware reciprocal / square root (v_rcp_f32 / v_sqrt_f32, 1 ulp): the IEEE-exact `1.f / x`
+// and `sqrtf` expand to ~10 instructions each (v_div_scale x2, v_div_fmas, v_div_fixup, Newton
+// steps; denormal scaling around v_sqrt), which made the element-wise update kernels issue-heavy
+// (AdamW: 54 instructions per element). Their results are rounded to bf16 / fp16 (8 / 11-bit
+// mantissas) or kept as fp32 moments where a 1-ulp difference is far below the update's own noise.
+// On this power-capped chip (profiles/r3_power_step.log) every instruction a streaming kernel
+// does not issue is power the concurrent GEMMs can spend.
+__device__ __forceinline__ float fast_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
+__device__ __forceinline__ float fast_sqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
+// logistic sigmoid; `exact` (uniform): IEEE division instead of v_rcp_f32 (FT_EXACT_MATH A/B)
+__device__ __forceinline__ float sigmoid_f(float x, bool exact) {
+  const float d = 1.f + __expf(-x);
+  return exact ? 1.f / d : fast_rcp(d);
+}
+
 __device__ __forceinline__ float bf2f(bf16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
 
 __device__ __forceinline__ bf16_t f2bf(float f) {

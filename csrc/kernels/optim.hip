@@ -132,7 +132,7 @@ __global__ __launch_bounds__(256) void adamw_kernel(typename P::T* __restrict__ 
                                                     float eps, float wd, float inv_bc1,
                                                     float inv_sqrt_bc2,
                                                     const float* __restrict__ stats,
-                                                    const float* __restrict__ hyper) {
+                                                    const float* __restrict__ hyper, int exact) {
   if (stats[2] != 0.f) return;  // non-finite gradient norm: skip the whole update
   if (hyper != nullptr) {
     // [lr, 1/bc1, 1/sqrt(bc2)] from device memory: a HIP-graph replay of the optimizer reads
@@ -157,8 +157,13 @@ __global__ __launch_bounds__(256) void adamw_kernel(typename P::T* __restrict__ 
       pf[j] *= decay;
       mf[j] += (gj - mf[j]) * (1.f - beta1);
       vf[j] = vf[j] * beta2 + (1.f - beta2) * gj * gj;
-      const float denom = sqrtf(vf[j]) * inv_sqrt_bc2 + eps;
-      pf[j] -= step * mf[j] / denom;
+      if (exact) {  // IEEE division / sqrt (FT_EXACT_MATH A/B)
+        const float denom = sqrtf(vf[j]) * inv_sqrt_bc2 + eps;
+        pf[j] -= step * mf[j] / denom;
+      } else {
+        const float denom = fast_sqrt(vf[j]) * inv_sqrt_bc2 + eps;
+        pf[j] -= step * mf[j] * fast_rcp(denom);
+      }
     }
     V8<P, NT>::store(p + i * 8, pf);
     V8<S, NT>::store(m + i * 8, mf);
@@ -249,12 +254,12 @@ void adamw_(const at::Tensor& p, const at::Tensor& g, const at::Tensor& m, const
       hipLaunchKernelGGL((adamw_kernel<P, S, true>), grid, block, 0, ft_stream(), mptr<PT>(p),
                          cptr<PT>(g), mptr<ST>(m), mptr<ST>(v), n8, (float)lr, (float)beta1,
                          (float)beta2, (float)eps, (float)wd, inv_bc1, inv_sqrt_bc2,
-                         cptr<float>(stats), hp);
+                         cptr<float>(stats), hp, (int)ft_exact_math());
     else
       hipLaunchKernelGGL((adamw_kernel<P, S, false>), grid, block, 0, ft_stream(), mptr<PT>(p),
                          cptr<PT>(g), mptr<ST>(m), mptr<ST>(v), n8, (float)lr, (float)beta1,
                          (float)beta2, (float)eps, (float)wd, inv_bc1, inv_sqrt_bc2,
-                         cptr<float>(stats), hp);
+                         cptr<float>(stats), hp, (int)ft_exact_math());
   };
   FT_DISPATCH_E(p.scalar_type(), {
     if (m.scalar_type() == at::kFloat) go(E{}, EF32{});

@@ -11,11 +11,20 @@
 
 namespace {
 
-__device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }
+
+// d/dg, d/du of silu(g) * u given the upstream d, with every fma explicit so the element-wise and
+// the tiled kernels round identically (the contraction the compiler picks otherwise differs by
+// kernel once the division is a plain v_rcp_f32).
+__device__ __forceinline__ void swiglu_grad(float g, float u, float d, bool exact, float& dg, float& du) {
+  const float s = sigmoid_f(g, exact);
+  const float silu = g * s;
+  du = d * silu;
+  dg = (d * u) * fmaf(silu, 1.f - s, s);
+}
 
 template <class E>
 __global__ __launch_bounds__(256) void swiglu_fwd_kernel(const typename E::T* __restrict__ gu,
-                                                         typename E::T* __restrict__ a, long T, int F) {
+                                                         typename E::T* __restrict__ a, long T, int F, int exact) {
   const int vpr = F >> 3;
   const long total = T * vpr;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
@@ -26,7 +35,7 @@ __global__ __launch_bounds__(256) void swiglu_fwd_kernel(const typename E::T* __
     ld8<E>(gu + row * 2 * F + col, g);
     ld8<E>(gu + row * 2 * F + F + col, u);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = g[j] * sigmoidf_(g[j]) * u[j];
+    for (int j = 0; j < 8; ++j) o[j] = g[j] * sigmoid_f(g[j], exact) * u[j];
     st8<E>(a + row * F + col, o);
   }
 }
@@ -34,7 +43,7 @@ __global__ __launch_bounds__(256) void swiglu_fwd_kernel(const typename E::T* __
 template <class E>
 __global__ __launch_bounds__(256) void swiglu_bwd_kernel(const typename E::T* __restrict__ da,
                                                          const typename E::T* __restrict__ gu,
-                                                         typename E::T* __restrict__ dgu, long T, int F) {
+                                                         typename E::T* __restrict__ dgu, long T, int F, int exact) {
   const int vpr = F >> 3;
   const long total = T * vpr;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
@@ -47,10 +56,7 @@ __global__ __launch_bounds__(256) void swiglu_bwd_kernel(const typename E::T* __
     ld8<E>(da + row * F + col, d);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const float s = sigmoidf_(g[j]);
-      const float silu = g[j] * s;
-      du[j] = d[j] * silu;
-      dg[j] = d[j] * u[j] * (s + silu * (1.f - s));
+      swiglu_grad(g[j], u[j], d[j], exact, dg[j], du[j]);
     }
     st8<E>(dgu + row * 2 * F + col, dg);
     st8<E>(dgu + row * 2 * F + F + col, du);
@@ -65,7 +71,7 @@ constexpr int TT = 64;
 
 __global__ __launch_bounds__(256) void swiglu_fwd_t_kernel(const bf16_t* __restrict__ gu,
                                                            bf16_t* __restrict__ a,
-                                                           bf16_t* __restrict__ aT, int T, int F) {
+                                                           bf16_t* __restrict__ aT, int T, int F, int exact) {
   __shared__ bf16_t tile[TT][TT + 2];
   const int tilesF = F / TT;
   const int r0 = (blockIdx.x / tilesF) * TT, c0 = (blockIdx.x % tilesF) * TT;
@@ -78,7 +84,7 @@ __global__ __launch_bounds__(256) void swiglu_fwd_t_kernel(const bf16_t* __restr
     unpack8(*reinterpret_cast<const uint4*>(gu + base), g);
     unpack8(*reinterpret_cast<const uint4*>(gu + base + F), u);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = g[j] * sigmoidf_(g[j]) * u[j];
+    for (int j = 0; j < 8; ++j) o[j] = g[j] * sigmoid_f(g[j], exact) * u[j];
     const uint4 v = pack8(o);
     if (a != nullptr) *reinterpret_cast<uint4*>(a + (long)(r0 + row) * F + c0 + seg * 8) = v;
     const bf16_t* e = reinterpret_cast<const bf16_t*>(&v);
@@ -105,7 +111,7 @@ __global__ __launch_bounds__(256) void swiglu_fwd_t_kernel(const bf16_t* __restr
 __global__ __launch_bounds__(256) void swiglu_bwd_rt_kernel(const bf16_t* __restrict__ da,
                                                             const bf16_t* __restrict__ gu,
                                                             bf16_t* __restrict__ dgu,
-                                                            bf16_t* __restrict__ dguT, int T, int F) {
+                                                            bf16_t* __restrict__ dguT, int T, int F, int exact) {
   const int lane = threadIdx.x & 63;
   const int tilesF = F / TT;
   const int tile = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -129,10 +135,7 @@ __global__ __launch_bounds__(256) void swiglu_bwd_rt_kernel(const bf16_t* __rest
     unpack8(D[i], d);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const float sg = sigmoidf_(g[j]);
-      const float silu = g[j] * sg;
-      du[j] = d[j] * silu;
-      dg[j] = d[j] * u[j] * (sg + silu * (1.f - sg));
+      swiglu_grad(g[j], u[j], d[j], exact, dg[j], du[j]);
       og[i][j] = f2bf(dg[j]);
       ou[i][j] = f2bf(du[j]);
     }
@@ -181,7 +184,7 @@ at::Tensor swiglu_fwd(const at::Tensor& gu) {
   if (work > 0)
     FT_DISPATCH_E(gu.scalar_type(),
                   hipLaunchKernelGGL(swiglu_fwd_kernel<E>, dim3(grid_for(work)), dim3(256), 0, ft_stream(),
-                                     cptr<typename E::T>(gu), mptr<typename E::T>(a), T, F));
+                                     cptr<typename E::T>(gu), mptr<typename E::T>(a), T, F, (int)ft_exact_math()));
   FT_LAUNCH_CHECK();
   return a;
 }
@@ -203,7 +206,7 @@ at::Tensor swiglu_bwd(const at::Tensor& da, const at::Tensor& gu) {
     FT_DISPATCH_E(gu.scalar_type(),
                   hipLaunchKernelGGL(swiglu_bwd_kernel<E>, dim3(grid_for(work)), dim3(256), 0, ft_stream(),
                                      cptr<typename E::T>(da), cptr<typename E::T>(gu), mptr<typename E::T>(dgu),
-                                     T, F));
+                                     T, F, (int)ft_exact_math()));
   FT_LAUNCH_CHECK();
   return dgu;
 }
@@ -222,7 +225,8 @@ std::tuple<at::Tensor, at::Tensor> swiglu_fwd_t(const at::Tensor& gu, bool plain
   auto aT = at::empty({F, T}, gu.options());
   if (T > 0)
     hipLaunchKernelGGL(swiglu_fwd_t_kernel, dim3((T / TT) * (F / TT)), dim3(256), 0, ft_stream(),
-                       cptr<bf16_t>(gu), plain ? mptr<bf16_t>(a) : nullptr, mptr<bf16_t>(aT), T, F);
+                       cptr<bf16_t>(gu), plain ? mptr<bf16_t>(a) : nullptr, mptr<bf16_t>(aT), T, F,
+                       (int)ft_exact_math());
   FT_LAUNCH_CHECK();
   return {a, aT};
 }
@@ -244,12 +248,16 @@ std::tuple<at::Tensor, at::Tensor> swiglu_bwd_t(const at::Tensor& da, const at::
   if (T > 0)
     hipLaunchKernelGGL(swiglu_bwd_rt_kernel, dim3((tiles + 3) / 4), dim3(256), 0, ft_stream(),
                        cptr<bf16_t>(da), cptr<bf16_t>(gu), plain ? mptr<bf16_t>(dgu) : nullptr,
-                       mptr<bf16_t>(dguT), T, F);
+                       mptr<bf16_t>(dguT), T, F, (int)ft_exact_math());
   FT_LAUNCH_CHECK();
   return {dgu, dguT};
 }
 
+// Same-process A/B of the IEEE-exact vs hardware reciprocal / sqrt (see ft_exact_math).
+void set_exact_math(bool on) { ft_exact_math() = on; }
+
 TORCH_LIBRARY_FRAGMENT(ftamd, m) {
+  m.def("set_exact_math(bool on) -> ()", &set_exact_math);
   m.def("swiglu_fwd_t(Tensor gu, bool plain=True) -> (Tensor, Tensor)", &swiglu_fwd_t);
   m.def("swiglu_bwd_t(Tensor da, Tensor gu, bool plain=True) -> (Tensor, Tensor)", &swiglu_bwd_t);
   m.def("swiglu_fwd(Tensor gu) -> Tensor", &swiglu_fwd);

@@ -1,12 +1,25 @@
 // Host-side glue between at::Tensor and the gfx950 kernels.
 #pragma once
 
+#include <cstdlib>
+
 #include <ATen/ATen.h>
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 #include <c10/core/DeviceGuard.h>
 #include <torch/library.h>
 
 #include "common.h"
+
+// FT_EXACT_MATH=1: IEEE-exact division / sqrt in the element-wise update kernels (AdamW, SwiGLU)
+// instead of the hardware v_rcp_f32 / v_sqrt_f32 (common.h fast_rcp); same-process A/B through
+// torch.ops.ftamd.set_exact_math.
+inline bool& ft_exact_math() {
+  static bool v = [] {
+    const char* e = std::getenv("FT_EXACT_MATH");
+    return e != nullptr && std::atoi(e) != 0;
+  }();
+  return v;
+}
 
 static inline hipStream_t ft_stream() {
   return at::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();

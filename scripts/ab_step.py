@@ -16,6 +16,7 @@ Knobs toggled between timing windows (alternating rounds, so box and clock drift
   w4fwd — forward x W^T GEMMs with narrow tiles on the 4-wave hand GEMM (csrc/kernels/gemm_w4.hip)
   w4dw  — weight gradients on the 4-wave hand GEMM (transposed operands)
   notrans — weight gradients on hipBLASLt from the row-major operands (no transpose kernels)
+  fastmath — AdamW / SwiGLU with the hardware v_rcp_f32 / v_sqrt_f32 instead of IEEE division/sqrt
 Usage: python scripts/ab_step.py [--steps 8] [--rounds 3] [--configs gemm,dw ...]
 """
 from __future__ import annotations
@@ -115,7 +116,8 @@ def main():
                "hand_dw_wo": shapes("dw:4096x4096x2048"), "dw": Fx.set_dw_stream, "tonly": Fx.set_ffn_t_only,
                "dkdv2": kernels().flash_set_dkdv2, "prio": set_prio, "sumsq_end": ddp_mod.set_sumsq_at_end,
                "qkvrope": Fx.set_qkv_rope, "w4fwd": Fx.set_w4_fwd, "w4dw": Fx.set_w4_dw,
-               "notrans": lambda on: setattr(Fx, "_DW_MODE", "none" if on else "auto")}
+               "notrans": lambda on: setattr(Fx, "_DW_MODE", "none" if on else "auto"),
+               "fastmath": lambda on: (torch.cuda.synchronize(), kernels().set_exact_math(not on))}
     configs = list(itertools.product([False, True], repeat=len(knobs)))
 
     def apply(cfg):

@@ -9,14 +9,15 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from fault_tolerant_llm_training_amd._native import kernels
 
 K = kernels()
-# python scripts/flash_bench.py [S Hq Hkv D]  (default: the Llama-3-8B layer, S=2048, 32/8 heads, d=128)
+# python scripts/flash_bench.py [S Hq Hkv D [B]]  (default: the Llama-3-8B layer, S=2048, 32/8 heads, d=128)
 S, Hq, Hkv, D = (int(v) for v in sys.argv[1:5]) if len(sys.argv) >= 5 else (2048, 32, 8, 128)
-print(f"S={S} Hq={Hq} Hkv={Hkv} D={D}")
-qkv = torch.randn(S, (Hq + 2 * Hkv) * D, device="cuda").bfloat16()
-qk = torch.randn(S, (Hq + Hkv) * D, device="cuda").bfloat16()
-do = torch.randn(S, Hq * D, device="cuda").bfloat16()
+Bt = int(sys.argv[5]) if len(sys.argv) >= 6 else 1
+print(f"S={S} Hq={Hq} Hkv={Hkv} D={D}" + (f" B={Bt}" if Bt > 1 else ""))
+qkv = torch.randn(Bt * S, (Hq + 2 * Hkv) * D, device="cuda").bfloat16()
+qk = torch.randn(Bt * S, (Hq + Hkv) * D, device="cuda").bfloat16()
+do = torch.randn(Bt * S, Hq * D, device="cuda").bfloat16()
 o, lse = K.flash_fwd(qk, qkv, S, Hq, Hkv, D)
-unit = 2 * (S * S / 2) * D * Hq  # flops of one causal [S x S/2 x D] matmul over all heads
+unit = 2 * (S * S / 2) * D * Hq * Bt  # flops of one causal [S x S/2 x D] matmul over all heads
 
 
 def t(fn, it=20):

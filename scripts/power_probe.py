@@ -148,6 +148,12 @@ def main():
     phase("adamw", [adamw])
     phase("gemm chain + adamw (2 str)", [gemms, adamw])
     phase("gemm chain", [gemms])
+    if hasattr(K, "set_exact_math"):  # AdamW with IEEE division / sqrt vs the hardware rcp / sqrt
+        for exact in (True, False, True, False):
+            K.set_exact_math(exact)
+            phase(f"adamw exact={int(exact)}", [adamw])
+            phase(f"gemm chain + adamw exact={int(exact)}", [gemms, adamw])
+        K.set_exact_math(False)
     smp.stop_ = True
 
 
