@@ -1387,8 +1387,10 @@ int g_fwd_split = [] {
   return e == nullptr ? -1 : std::atoi(e);
 }();
 
-// Software-pipelined forward (flash_fwd_pipe_kernel) for the unsplit grids: 1 on, 0 off
-// (FT_FLASH_FWD_PIPE / flash_set_fwd_pipe, for A/B).
+// Software-pipelined forward (flash_fwd_pipe_kernel) for the unsplit grids: >= 1 on, 0 off
+// (FT_FLASH_FWD_PIPE / flash_set_fwd_pipe, for A/B). (A balanced variant — one 8-wave block per
+// query-tile pair, the long tile's keys split between the halves and merged in LDS — ran slower:
+// 60.0 vs 53.3 us at S = 2048, profiles/r3_flash_fwd_pipe.log.)
 int g_fwd_pipe = [] {
   const char* e = std::getenv("FT_FLASH_FWD_PIPE");
   return e == nullptr ? 1 : std::atoi(e);
@@ -1479,7 +1481,7 @@ std::tuple<at::Tensor, at::Tensor> flash_fwd(const at::Tensor& qk, const at::Ten
   hipLaunchKernelGGL((flash_fwd_pipe_kernel<E, DD, 4>), grid, block, 0, ft_stream(), cptr<bf16_t>(qk), \
                      cptr<bf16_t>(qkv), mptr<bf16_t>(out), mptr<float>(lse), B, (int)S, (int)Hq,   \
                      (int)Hkv, sl2, ldqk)
-  const bool pipe = !split && g_fwd_pipe == 1;
+  const bool pipe = !split && g_fwd_pipe >= 1;
   FT_DISPATCH_E16(qk.scalar_type(), {
     if (D == 128) {
       if (split) FT_FWD(128, 2); else if (pipe) FT_FWD_PIPE(128); else FT_FWD(128, 1);

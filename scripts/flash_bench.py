@@ -42,10 +42,10 @@ if hasattr(K, "flash_set_fwd_split"):  # forward key split forced off / on (defa
         print(f"fwd key split {'on ' if v else 'off'} {tf:7.1f} us  {2 * unit / tf / 1e6:6.0f} TF/s")
     K.flash_set_fwd_split(-1)
 if hasattr(K, "flash_set_fwd_pipe"):  # software-pipelined forward off / on (default: on)
-    for v in (0, 1):
+    for v, name in ((0, "unpipelined"), (1, "pipelined")):
         K.flash_set_fwd_pipe(v)
         tf = t(lambda: K.flash_fwd(qk, qkv, S, Hq, Hkv, D))
-        print(f"fwd pipelined {'on ' if v else 'off'} {tf:7.1f} us  {2 * unit / tf / 1e6:6.0f} TF/s")
+        print(f"fwd {name:26s} {tf:7.1f} us  {2 * unit / tf / 1e6:6.0f} TF/s")
     K.flash_set_fwd_pipe(1)
 for mode, name in ((0, "bwd atomics"), (1, "bwd deterministic"), (2, "bwd no-atomic (racy, timing only)")):
     tb = t(lambda: K.flash_bwd(do, qk, qkv, o, lse, S, Hq, Hkv, D, mode))

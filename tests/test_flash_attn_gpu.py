@@ -152,7 +152,7 @@ def test_flash_fwd_pipe_matches(B, S, Hq, Hkv, D):
         K.flash_set_fwd_split(0)
         K.flash_set_fwd_pipe(0)
         o0, l0 = K.flash_fwd(qk, qkv, S, Hq, Hkv, D)
-        K.flash_set_fwd_pipe(1)
+        K.flash_set_fwd_pipe(2)
         o1, l1 = K.flash_fwd(qk, qkv, S, Hq, Hkv, D)
     finally:
         K.flash_set_fwd_split(-1)
