@@ -616,7 +616,9 @@ def _qkv_rope_ok(x2: torch.Tensor, w: torch.Tensor, d: int) -> bool:
     if not (_QKV_ROPE and _GEMM_MODE != "blas" and x2.is_cuda and x2.dtype in _W4_DTYPES
             and w.dtype == x2.dtype):
         return False
-    return d % 8 == 0 and _w4_fits(x2, w)
+    # K >= 2048 (the 8B-class projections): at GPT-2 sizes (K = 768 / 1024) the epilogue kernel
+    # loses ~1 % of the step to hipBLASLt + the RoPE kernel (profiles/r3_gpt2_w4_ab.log)
+    return d % 8 == 0 and x2.shape[1] >= 2048 and _w4_fits(x2, w)
 
 
 class QKVRopeFn(torch.autograd.Function):
