@@ -126,10 +126,34 @@ def _w4_ok(x2: torch.Tensor, w: torch.Tensor) -> bool:
     return _W4_FWD and _w4_fits(x2, w, _W4_FWD_MAX_NJ)
 
 
+# GPT-2-sized forward products on the 128 x 128-tile kernel (csrc/kernels/gemm_s.hip): K <= 1024
+# and at least 256 output tiles. Alone (graph-timed) it runs GPT-2-small qkv 1.20x / w13 1.10x,
+# -medium qkv 1.05x / w13 1.15x hipBLASLt (profiles/r3_gemm_s_vs_hipblaslt.log), but inside the
+# graph-replayed step it measured 0.99-1.00x (its two workgroups per CU share the CUs with the
+# pipelined optimizer and the dW stream; profiles/r3_gpt2_s_ab.log): opt-in, FT_GEMM_S=1.
+_GEMM_S = os.environ.get("FT_GEMM_S", "0") == "1"
+
+
+def set_gemm_s(on: bool) -> None:
+    global _GEMM_S
+    _GEMM_S = bool(on)
+
+
+def _s_ok(x2: torch.Tensor, w: torch.Tensor) -> bool:
+    if not (_GEMM_S and _GEMM_MODE != "blas" and x2.is_cuda and x2.dtype in _W4_DTYPES and w.dtype == x2.dtype):
+        return False
+    T, K = x2.shape
+    N = w.shape[0]
+    return T % 128 == 0 and N % 128 == 0 and K % 64 == 0 and K <= 1024 and (T // 128) * (N // 128) >= 256
+
+
 def mm_fwd(x2: torch.Tensor, w: torch.Tensor, residual: Optional[torch.Tensor] = None) -> torch.Tensor:
     """y = x2 @ w^T (+ residual): x2 [T, K], w [N, K] (nn.Linear layout)."""
     T, K = x2.shape
     N = w.shape[0]
+    if _s_ok(x2, w):
+        return kernels().gemm_nt_s(x2.contiguous(), w, None,
+                                   None if residual is None else residual.reshape(T, N).contiguous(), 1)
     if _w4_ok(x2, w):
         return kernels().gemm_nt_w4(x2.contiguous(), w, None,
                                     None if residual is None else residual.reshape(T, N).contiguous(), 0)

@@ -168,3 +168,41 @@ def test_weight_grad_on_w4(T, N, Kd):
         assert ((buf.view(N, Kd).float() - 2 * ref).norm() / (2 * ref).norm()).item() < 6e-3
     finally:
         Fx.set_w4_dw(old)
+
+
+@pytest.mark.parametrize("ks", [0, 1, 2, 4])
+@pytest.mark.parametrize("M,N,K", [(128, 128, 64), (2048, 768, 768), (2048, 2304, 768), (2048, 768, 2048),
+                                   (256, 384, 4096), (2048, 1024, 2816)])
+def test_gemm_s_tiles(M, N, K, ks):
+    """128 x 128-tile GEMM (csrc/kernels/gemm_s.hip) incl. split-K, vs fp32; residual; bitwise
+    reproducible (the split-K slices are summed in a fixed order by the last-arriving workgroup)."""
+    from fault_tolerant_llm_training_amd._native import kernels
+
+    K_ = kernels()
+    torch.manual_seed(M + N + K + ks)
+    a = (torch.rand(M, K, device="cuda") * 2 - 1).bfloat16()
+    b = (torch.rand(N, K, device="cuda") * 2 - 1).bfloat16()
+    ref = a.float() @ b.float().t()
+    out = K_.gemm_nt_s(a, b, None, None, ks)
+    assert ((out.float() - ref).norm() / ref.norm()).item() < 4e-3
+    r = (torch.rand(M, N, device="cuda") * 2 - 1).bfloat16()
+    out = K_.gemm_nt_s(a, b, None, r, ks)
+    ref = ref + r.float()
+    assert ((out.float() - ref).norm() / ref.norm()).item() < 4e-3
+    for _ in range(3):
+        o2 = torch.empty_like(out)
+        K_.gemm_nt_s(a, b, o2, r, ks)
+        assert torch.equal(o2, out)
+
+
+def test_gemm_s_fp16():
+    from fault_tolerant_llm_training_amd._native import kernels
+
+    K_ = kernels()
+    torch.manual_seed(7)
+    a = (torch.rand(512, 768, device="cuda") * 2 - 1).half()
+    b = (torch.rand(384, 768, device="cuda") * 2 - 1).half()
+    ref = a.float() @ b.float().t()
+    out = K_.gemm_nt_s(a, b, None, None, 0)
+    assert out.dtype == torch.float16
+    assert ((out.float() - ref).norm() / ref.norm()).item() < 2e-3
