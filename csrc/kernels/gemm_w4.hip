@@ -54,7 +54,7 @@ constexpr int PIECE = 1024;  // one LDS-DMA wave-instruction: 8 image rows of 12
 constexpr int FS = 2 * PIECE;  // one 16-row fragment
 constexpr int OPA = 32 * PIECE;  // A image: 256 rows
 
-enum W4Epi : int { W4_STORE = 0, W4_RES = 1, W4_ROPE = 2 };
+enum W4Epi : int { W4_STORE = 0, W4_RES = 1, W4_ROPE = 2, W4_SWIGLU = 3 };
 
 __device__ __forceinline__ unsigned lds_u32(const void* p) {
   return (unsigned)(uintptr_t)((const __attribute__((address_space(3))) char*)p);
@@ -122,6 +122,13 @@ struct W4Args {
   int rope_cols;         // RoPE: columns [0, rope_cols) are rotated (Hq + Hkv heads)
   int rope_hd;           // head dim
   int rope_seq;          // sequence length (position = row % seq)
+  // SwiGLU epilogue (W4_SWIGLU): b = [w1; w3] ([2F, K]); tile tn covers features
+  // [tn * 16 NJ, +16 NJ) of BOTH halves (B image rows = that slice of w1, then of w3), so the
+  // tile holds g and u of the same features: c = gu [M, 2F], a = silu(g) u [M, F], a^T [F, M]
+  int ffn;               // F
+  bf16_t* act;           // a
+  bf16_t* actT;          // a^T
+  int exact;             // IEEE division in the sigmoid (FT_EXACT_MATH), as swiglu_fwd_t
 };
 
 __device__ __forceinline__ void tile_of(int bid, int tiles_m, int tiles_n, int& tm, int& tn) {
@@ -242,6 +249,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(W4Args p) {
   int tm, tn;
   tile_of(blockIdx.x, p.tiles_m, p.tiles_n, tm, tn);
   const int m0 = tm * BM, n0 = tn * BN;
+  const int f0 = tn * NW;  // W4_SWIGLU: first feature of the tile (NW features of w1 and of w3)
   const int nk = p.K / BK;
 
   // LDS-DMA sources: instruction q of wave w covers image rows (q * 4 + w) * 8 + (lane >> 3);
@@ -249,12 +257,14 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(W4Args p) {
   Ctx c;
   c.wid = wid;
   c.srdA = make_srd(p.a + (long)m0 * p.lda);
-  c.srdB = make_srd(p.b + (long)n0 * p.ldb);
+  c.srdB = make_srd(EPI == W4_SWIGLU ? p.b : p.b + (long)n0 * p.ldb);
   const int lrow = wid * 8 + (lane >> 3), lch = (lane & 7) ^ (lane >> 3);
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
     c.voA[q] = (unsigned)(((q * 32 + lrow) * p.lda + lch * 8) * 2);
-    c.voB[q] = (unsigned)(((q * 32 + lrow) * p.ldb + lch * 8) * 2);
+    const int r = q * 32 + lrow;  // B image row
+    const long src = EPI == W4_SWIGLU ? (r < 16 * NJ ? f0 + r : (long)p.ffn + f0 + (r - 16 * NJ)) : r;
+    c.voB[q] = (unsigned)((src * p.ldb + lch * 8) * 2);
   }
   c.lds0 = __builtin_amdgcn_readfirstlane(lds_u32(smem));
   // fragment reads: lane reads row r0 + (lane & 15), chunk (kk * 4 + (lane >> 4)) ^ (lane & 7)
@@ -334,7 +344,8 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(W4Args p) {
       const int row = rr * 4 + (lane >> 4);
       uint4 v = *reinterpret_cast<const uint4*>(wl + row * 256 + ((cc ^ (row & 15)) << 4));
       const long gm = m0 + wm * 128 + row;
-      const int gn = n0 + wn * NW + cc * 8;
+      // W4_SWIGLU: wave column half 0 holds g (gu columns [0, F)), half 1 holds u ([F, 2F))
+      const int gn = EPI == W4_SWIGLU ? (wn ? p.ffn : 0) + f0 + cc * 8 : n0 + wn * NW + cc * 8;
       if constexpr (EPI == W4_RES) {
         float a[8], r[8];
         unpack8e<E>(v, a);
@@ -367,6 +378,60 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(W4Args p) {
       *reinterpret_cast<uint4*>(p.c + gm * p.ldc + gn) = v;
     }
   }
+  if constexpr (EPI == W4_SWIGLU) {
+    // a = silu(g) * u from the parked bf16 g / u quadrants (the values just stored to gu, so a is
+    // bitwise what swiglu_fwd_t computes from gu): wave (wm, wn) takes rows [64 wn, 64 wn + 64) of
+    // its row half, writes a row-major and back over g in LDS, then all waves store a^T
+    __syncthreads();
+    char* gl = smem + (wm * 2) * 32768;      // g quadrant of this row half
+    char* ul = smem + (wm * 2 + 1) * 32768;  // u quadrant
+    if (cc < 2 * NJ) {
+#pragma unroll 4
+      for (int rr = 0; rr < 16; ++rr) {
+        const int row = wn * 64 + rr * 4 + (lane >> 4);
+        const int off = row * 256 + ((cc ^ (row & 15)) << 4);
+        float g8[8], u8[8], a8[8];
+        unpack8e<E>(*reinterpret_cast<const uint4*>(gl + off), g8);
+        unpack8e<E>(*reinterpret_cast<const uint4*>(ul + off), u8);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) a8[q] = g8[q] * sigmoid_f(g8[q], p.exact) * u8[q];
+        const uint4 av = pack8e<E>(a8);
+        *reinterpret_cast<uint4*>(p.act + (m0 + wm * 128 + row) * (long)p.ffn + f0 + cc * 8) = av;
+        *reinterpret_cast<uint4*>(gl + off) = av;
+      }
+    }
+    __syncthreads();
+    // a^T [F, M]: a thread takes 8 tokens x 8 features (8 row-chunk LDS reads, feature chunk
+    // fastest across lanes: distinct XOR-swizzled chunks, conflict-free), transposes the block in
+    // registers and stores 8 16-B pieces (8 tokens of one feature each)
+    constexpr int CH = 2 * NJ;  // 8-feature chunks per tile row
+    for (int k = tid; k < 2 * 16 * CH; k += NT) {
+      const int fc = k % CH, tg = (k / CH) % 16, hf = k / (16 * CH);
+      const char* al = smem + (hf * 2) * 32768;  // a of row half hf (written over g)
+      uint16_t e[8][8];                          // [token][feature]
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int row = tg * 8 + i;
+        const uint4 v = *reinterpret_cast<const uint4*>(al + row * 256 + ((fc ^ (row & 15)) << 4));
+        const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          e[i][2 * q] = (uint16_t)(wv[q] & 0xffffu);
+          e[i][2 * q + 1] = (uint16_t)(wv[q] >> 16);
+        }
+      }
+      bf16_t* dst = p.actT + (long)(f0 + fc * 8) * p.M + m0 + hf * 128 + tg * 8;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        uint4 o;
+        o.x = e[0][j] | ((uint32_t)e[1][j] << 16);
+        o.y = e[2][j] | ((uint32_t)e[3][j] << 16);
+        o.z = e[4][j] | ((uint32_t)e[5][j] << 16);
+        o.w = e[6][j] | ((uint32_t)e[7][j] << 16);
+        *reinterpret_cast<uint4*>(dst + (long)j * p.M) = o;
+      }
+    }
+  }
 }
 
 template <class E, int NJ>
@@ -376,6 +441,8 @@ void launch_nj(const W4Args& p, int epi, hipStream_t st) {
     hipLaunchKernelGGL((gemm_w4_kernel<E, NJ, W4_RES>), g, dim3(NT), 0, st, p);
   else if (epi == W4_ROPE)
     hipLaunchKernelGGL((gemm_w4_kernel<E, NJ, W4_ROPE>), g, dim3(NT), 0, st, p);
+  else if (epi == W4_SWIGLU)
+    hipLaunchKernelGGL((gemm_w4_kernel<E, NJ, W4_SWIGLU>), g, dim3(NT), 0, st, p);
   else
     hipLaunchKernelGGL((gemm_w4_kernel<E, NJ, W4_STORE>), g, dim3(NT), 0, st, p);
 }
@@ -509,6 +576,47 @@ at::Tensor gemm_qkv_rope_w4(const at::Tensor& x, const at::Tensor& w, const at::
   return c;
 }
 
+// Fused w1|w3 projection + SwiGLU (reference model.py:254 silu(w1 x) * w3 x): x [M, K],
+// w13 = [w1; w3] [2F, K] -> (gu [M, 2F] = x w13^T for the backward, a = silu(g) u [M, F],
+// a^T [F, M] for the w2 weight gradient). 224-column tiles: 112 features of w1 and the same 112 of
+// w3; M % 256, F % 112, K % 64.
+std::tuple<at::Tensor, at::Tensor, at::Tensor> gemm_swiglu_w4(const at::Tensor& x, const at::Tensor& w13) {
+  FT_CHECK_CUDA(x);
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kHalf, "gemm_swiglu_w4: bf16 / fp16");
+  TORCH_CHECK(w13.scalar_type() == x.scalar_type(), "gemm_swiglu_w4: x / w13 dtype mismatch");
+  FT_CHECK_CONTIG(x);
+  FT_CHECK_CONTIG(w13);
+  const long M = x.size(0), K = x.size(1), F2 = w13.size(0), F = F2 / 2;
+  constexpr int NJ = 7, NWC = 16 * NJ;
+  TORCH_CHECK(w13.size(1) == K && F2 % 2 == 0, "gemm_swiglu_w4: shape mismatch");
+  TORCH_CHECK(M % BM == 0 && F % NWC == 0 && K % BK == 0 && K >= BK, "gemm_swiglu_w4: M % 256, F % 112, K % 64 (got ",
+              M, " ", F, " ", K, ")");
+  TORCH_CHECK(M * K * 2 < (1L << 32) && F2 * K * 2 < (1L << 32), "gemm_swiglu_w4: operand over 4 GiB");
+  const at::DeviceGuard guard(x.device());
+  auto gu = at::empty({M, F2}, x.options());
+  auto a = at::empty({M, F}, x.options());
+  auto aT = at::empty({F, M}, x.options());
+  W4Args p{};
+  p.a = cptr<bf16_t>(x);
+  p.b = cptr<bf16_t>(w13);
+  p.c = mptr<bf16_t>(gu);
+  p.lda = K;
+  p.ldb = K;
+  p.ldc = F2;
+  p.M = M;
+  p.N = F2;
+  p.K = K;
+  p.tiles_m = M / BM;
+  p.tiles_n = F / NWC;
+  p.ffn = (int)F;
+  p.act = mptr<bf16_t>(a);
+  p.actT = mptr<bf16_t>(aT);
+  p.exact = (int)ft_exact_math();
+  launch(x.scalar_type(), NJ, p, W4_SWIGLU, ft_stream());
+  FT_LAUNCH_CHECK();
+  return {gu, a, aT};
+}
+
 int64_t gemm_w4_pick(int64_t M, int64_t N) { return pick_nj(M, N); }
 
 TORCH_LIBRARY_FRAGMENT(ftamd, m) {
@@ -517,4 +625,5 @@ TORCH_LIBRARY_FRAGMENT(ftamd, m) {
   m.def("gemm_qkv_rope_w4(Tensor x, Tensor w, Tensor cos, Tensor sin, int seq, int hq, int hkv, int d) -> Tensor",
         &gemm_qkv_rope_w4);
   m.def("gemm_w4_pick(int M, int N) -> int", &gemm_w4_pick);
+  m.def("gemm_swiglu_w4(Tensor x, Tensor w13) -> (Tensor, Tensor, Tensor)", &gemm_swiglu_w4);
 }

@@ -721,6 +721,31 @@ def set_ffn_t_only(on: bool) -> None:
     _FFN_T_ONLY = bool(on)
 
 
+# w1|w3 projection with SwiGLU in the GEMM epilogue (csrc/kernels/gemm_w4.hip, gemm_swiglu_w4): each
+# 224-column tile holds g and u of the same 112 features, the epilogue writes gu (for the backward),
+# a = silu(g) u and a^T, so the separate SwiGLU forward pass (a re-read of the [T, 2F] gu) is gone.
+# Opt-in (FT_W4_SWIGLU=1) until it measures faster in the step: first form 0.994x (profiles/r3_w4_swiglu_ab.log).
+_W4_SWIGLU = os.environ.get("FT_W4_SWIGLU", "0") == "1"
+
+
+def set_w4_swiglu(on: bool) -> None:
+    global _W4_SWIGLU
+    _W4_SWIGLU = bool(on)
+
+
+def _swiglu_w4_ok(x2: torch.Tensor, w13: torch.Tensor) -> bool:
+    """Fused path: bf16 on the GPU, w4 tile shapes (T % 256, F % 112, K % 64), at least half the
+    chip in tiles, and the transposed-operand weight-gradient path (which consumes a^T)."""
+    if not (_W4_SWIGLU and _W4_FWD and _GEMM_MODE != "blas" and x2.is_cuda and x2.dtype == torch.bfloat16
+            and w13.dtype == x2.dtype and not _FFN_T_ONLY):
+        return False
+    T, K = x2.shape
+    F = w13.shape[0] // 2
+    if T % 256 or K % 64 or F % 112 or (T // 256) * (F // 112) < 128:
+        return False
+    return _DW_MODE == "all" or (_DW_MODE != "none" and 2.0 * T * 2 * F * K >= _DW_MIN_FLOP)
+
+
 class FeedForwardFn(torch.autograd.Function):
     """x → [w1; w3] GEMM → SwiGLU → w2 GEMM as one autograd node (GPU, 64-multiple shapes).
 
@@ -734,13 +759,17 @@ class FeedForwardFn(torch.autograd.Function):
         K_ = kernels()
         D = x.shape[-1]
         x2 = x.reshape(-1, D)
-        gu = mm_fwd(x2, w13)
-        tn = _use_tn(gu, x2)
-        t_only = tn and _FFN_T_ONLY
-        if tn:
-            a, aT = K_.swiglu_fwd_t(gu, not t_only)
+        if _swiglu_w4_ok(x2, w13):
+            gu, a, aT = K_.gemm_swiglu_w4(x2.contiguous(), w13)
+            tn, t_only = True, False
         else:
-            a, aT = K_.swiglu_fwd(gu), None
+            gu = mm_fwd(x2, w13)
+            tn = _use_tn(gu, x2)
+            t_only = tn and _FFN_T_ONLY
+            if tn:
+                a, aT = K_.swiglu_fwd_t(gu, not t_only)
+            else:
+                a, aT = K_.swiglu_fwd(gu), None
         y = torch.mm(aT.t(), w2.t()) if t_only else mm_fwd(a, w2)
         ctx.sinks = (sink13, sink2)
         ctx.tn = tn

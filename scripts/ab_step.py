@@ -17,6 +17,8 @@ Knobs toggled between timing windows (alternating rounds, so box and clock drift
   w4dw  — weight gradients on the 4-wave hand GEMM (transposed operands)
   notrans — weight gradients on hipBLASLt from the row-major operands (no transpose kernels)
   fastmath — AdamW / SwiGLU with the hardware v_rcp_f32 / v_sqrt_f32 instead of IEEE division/sqrt
+  w4wide — the wide forward products (w13 at 224, the LM head at 256 columns) on the w4 GEMM too
+  w4swiglu — the w1|w3 GEMM on the w4 kernel with SwiGLU in its epilogue (no separate SwiGLU pass)
 Usage: python scripts/ab_step.py [--steps 8] [--rounds 3] [--configs gemm,dw ...]
 """
 from __future__ import annotations
@@ -117,7 +119,9 @@ def main():
                "dkdv2": kernels().flash_set_dkdv2, "prio": set_prio, "sumsq_end": ddp_mod.set_sumsq_at_end,
                "qkvrope": Fx.set_qkv_rope, "w4fwd": Fx.set_w4_fwd, "w4dw": Fx.set_w4_dw,
                "notrans": lambda on: setattr(Fx, "_DW_MODE", "none" if on else "auto"),
-               "fastmath": lambda on: (torch.cuda.synchronize(), kernels().set_exact_math(not on))}
+               "fastmath": lambda on: (torch.cuda.synchronize(), kernels().set_exact_math(not on)),
+               "w4swiglu": lambda on: (torch.cuda.synchronize(), Fx.set_w4_swiglu(on)),
+               "w4wide": lambda on: (torch.cuda.synchronize(), setattr(Fx, "_W4_FWD_MAX_NJ", 8 if on else 6))}
     configs = list(itertools.product([False, True], repeat=len(knobs)))
 
     def apply(cfg):

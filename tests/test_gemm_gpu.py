@@ -206,3 +206,24 @@ def test_gemm_s_fp16():
     out = K_.gemm_nt_s(a, b, None, None, 0)
     assert out.dtype == torch.float16
     assert ((out.float() - ref).norm() / ref.norm()).item() < 2e-3
+
+
+@pytest.mark.parametrize("M,F,K", [(256, 448, 64), (512, 1792, 640), (2048, 14336, 4096)])
+def test_gemm_swiglu_w4(M, F, K):
+    """w1|w3 GEMM with SwiGLU in the epilogue: gu equals the plain w4 GEMM bitwise (same MFMA order),
+    a / a^T equal swiglu_fwd_t of that gu bitwise, and all match fp32 (reference model.py:254)."""
+    from fault_tolerant_llm_training_amd._native import kernels
+
+    K_ = kernels()
+    torch.manual_seed(M + F + K)
+    x = (torch.rand(M, K, device="cuda") * 2 - 1).bfloat16()
+    w13 = ((torch.rand(2 * F, K, device="cuda") * 2 - 1) * (1.0 / K**0.5)).bfloat16()
+    gu, a, aT = K_.gemm_swiglu_w4(x, w13)
+    assert torch.equal(gu, K_.gemm_nt_w4(x, w13, None, None, 7))
+    a2, aT2 = K_.swiglu_fwd_t(gu, True)
+    assert torch.equal(a, a2) and torch.equal(aT, aT2)
+    ref = x.float() @ w13.float().t()
+    g, u = ref[:, :F], ref[:, F:]
+    aref = torch.nn.functional.silu(g) * u
+    assert ((gu.float() - ref).norm() / ref.norm()).item() < 4e-3
+    assert ((a.float() - aref).norm() / aref.norm()).item() < 1e-2
