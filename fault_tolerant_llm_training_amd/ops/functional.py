@@ -724,8 +724,9 @@ def set_ffn_t_only(on: bool) -> None:
 # w1|w3 projection with SwiGLU in the GEMM epilogue (csrc/kernels/gemm_w4.hip, gemm_swiglu_w4): each
 # 224-column tile holds g and u of the same 112 features, the epilogue writes gu (for the backward),
 # a = silu(g) u and a^T, so the separate SwiGLU forward pass (a re-read of the [T, 2F] gu) is gone.
-# Opt-in (FT_W4_SWIGLU=1) until it measures faster in the step: first form 0.994x (profiles/r3_w4_swiglu_ab.log).
-_W4_SWIGLU = os.environ.get("FT_W4_SWIGLU", "0") == "1"
+# 8B step 1.002x best / 1.003x median with a^T by in-register transposes (the first form, a^T
+# gathered by 2-byte LDS reads, was 0.994x): profiles/r3_w4_swiglu_ab.log. FT_W4_SWIGLU=0: GEMM + swiglu_fwd_t.
+_W4_SWIGLU = os.environ.get("FT_W4_SWIGLU", "1") != "0"
 
 
 def set_w4_swiglu(on: bool) -> None:
