@@ -419,3 +419,30 @@ def test_h2d_from_checkpoint_file(tmp_path):
     assert restore.STATS["file_bytes"] - before == src.numel() * 2
     assert torch.equal(dst.cpu(), src)
     restore.release()
+
+
+def test_exact_math_switch(K):
+    """AdamW / SwiGLU with the hardware v_rcp_f32 / v_sqrt_f32 (default) vs IEEE division and square
+    root (FT_EXACT_MATH / set_exact_math): the bf16 results agree except for rare 1-ulp rounding flips."""
+    torch.manual_seed(11)
+    n = 1 << 20
+    p = torch.randn(n, device="cuda").bfloat16()
+    g = (torch.randn(n, device="cuda") * 1e-2).bfloat16()
+    m = (torch.randn(n, device="cuda") * 1e-3).bfloat16()
+    v = (torch.rand(n, device="cuda") * 1e-5).bfloat16()
+    stats = torch.tensor([1.0, 1.0, 0.0], device="cuda")
+    gu = torch.randn(2048, 2 * 1024, device="cuda").bfloat16()
+    outs = {}
+    try:
+        for exact in (False, True):
+            K.set_exact_math(exact)
+            pp, mm, vv = p.clone(), m.clone(), v.clone()
+            K.adamw_(pp, g, mm, vv, stats, 1e-3, 0.9, 0.999, 1e-8, 0.01, 7)
+            outs[exact] = (pp, mm, vv, K.swiglu_fwd(gu))
+    finally:
+        K.set_exact_math(False)
+    for a, b in zip(outs[False], outs[True]):
+        diff = (a.float() - b.float()).abs()
+        ulp = b.float().abs() * 2.0 ** -7 + 1e-30
+        assert (diff <= ulp).all()
+        assert (diff > 0).float().mean().item() < 0.02
