@@ -65,6 +65,8 @@ def parse():
                          "of step k+1): for launch-bound presets (gpt2-small / gpt2-medium)")
     ap.add_argument("--device", default="cuda")
     ap.add_argument("--dp-mode", default="", choices=["", "allreduce", "zero1"])
+    ap.add_argument("--dp-reduce-dtype", default="native", choices=["native", "bf16", "fp32"],
+                    help="gradient collectives in the model dtype (default) or on an fp32 copy")
     ap.add_argument("--no-overlap", action="store_true", help="per-bucket optimizer as a serial phase (A/B)")
     ap.add_argument("--activation-checkpointing", type=int, default=0,
                     help="recompute this many blocks in backward (-1 = all): long-context runs")
@@ -100,13 +102,16 @@ def main():
     world = info.world_size
     if a.gpus != world and info.is_main:
         print(f"[bench] note: --gpus {a.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    # what the job really runs on: process-group size, one distinct GPU per rank (raises
+    # otherwise), peer access between every pair, RCCL version -- recorded in the JSON line
+    topo = fdist.topology_report(info, expected_world=a.gpus if world > 1 else None)
 
     margs = model_args_for(a.model, vocab_size=a.vocab_size, seq_len=a.seq_len)
     model = build_model(margs, dev, torch.bfloat16, seed=1234)
     if a.activation_checkpointing:
         model.set_activation_checkpointing(a.activation_checkpointing, recompute_attention=a.recompute_attention)
     red = GradReducer(model.flat, model.sinks_in_backward_order(), bucket_mb=a.bucket_mb,
-                      mode=a.dp_mode or None, overlap=not a.no_overlap)
+                      mode=a.dp_mode or None, overlap=not a.no_overlap, reduce_dtype=a.dp_reduce_dtype)
     if a.whole_buffer_optimizer and world == 1:
         for snk in list(model.flat.sinks.values()) + model.sinks_in_backward_order():
             snk.hook = None
@@ -157,9 +162,16 @@ def main():
             loss = graphed.prime(*data.batch(i, B))  # eager fwd/bwd of step i, then capture
         else:
             loss = step(i)
+    sampler = None
+    if dev.type == "cuda":
+        from fault_tolerant_llm_training_amd.utils.telemetry import start_sampler
+
+        sampler = start_sampler(dev.index or 0)
     _sync(dev)
     fdist.barrier()
     _sync(dev)
+    if sampler is not None:
+        sampler.on = True
     t0 = time.perf_counter()
     for i in range(a.steps):
         if graphed is not None:  # optimizer of step i-1 + forward/backward of step i
@@ -171,6 +183,9 @@ def main():
     fdist.barrier()
     _sync(dev)
     elapsed = time.perf_counter() - t0
+    if sampler is not None:
+        sampler.on = False
+        sampler.stop_ = True
     if graphed is not None:
         graphed.finish()  # the last backward's optimizer step (outside the timed window)
         opt.graph_mode = False
@@ -218,7 +233,21 @@ def main():
             (world - 1) * B * K * S * (margs.dim * model.flat.grads.element_size() + 8) / 1e9, 3)
         if red.sparse_embedding else 0.0,
         "recompute_layers": model.recompute_layers,
+        "world_size": topo["world_size"],
+        "distinct_devices": topo["distinct_devices"],
+        "device_ids": [d["id"] for d in topo["devices"]],
+        "peer_access_all_pairs": topo["peer_access_all_pairs"],
+        "rccl_version": topo["rccl_version"],
     }
+    if sampler is not None:
+        # board power / shader clock over the timed region (rank 0's GPU): the step runs at the
+        # power limit, so these tell a hotter or lower-clocked box from slower code
+        out.update(sampler.summary())
+        sc = out.get("sclk_mhz_p50")
+        if sc:
+            out["ms_per_step_at_2000mhz"] = round(ms * sc / 2000.0, 2)
+    if a.dp_reduce_dtype == "fp32":
+        out["dp_reduce_dtype"] = "fp32"
     if graphed is not None:
         out["hip_graph"] = True
     if dev.type == "cuda":

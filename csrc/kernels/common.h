@@ -34,6 +34,16 @@ __device__ __forceinline__ float sigmoid_f(float x, bool exact) {
   return exact ? 1.f / d : fast_rcp(d);
 }
 
+// d/dg, d/du of silu(g) * u given the upstream d, with every fma explicit so the element-wise
+// kernels (swiglu.hip) and the GEMM epilogue (gemm_w4.hip) round identically (the contraction the
+// compiler picks otherwise differs by kernel once the division is a plain v_rcp_f32).
+__device__ __forceinline__ void swiglu_grad(float g, float u, float d, bool exact, float& dg, float& du) {
+  const float s = sigmoid_f(g, exact);
+  const float silu = g * s;
+  du = d * silu;
+  dg = (d * u) * fmaf(silu, 1.f - s, s);
+}
+
 __device__ __forceinline__ float bf2f(bf16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
 
 __device__ __forceinline__ bf16_t f2bf(float f) {

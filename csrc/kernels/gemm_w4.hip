@@ -1,7 +1,13 @@
 // 4-wave bf16 / fp16 GEMM for gfx950 with an instruction-level schedule (the "w4" kernel).
 //
-//   C[M, N] = sum_k A(m, k) * B(k, n)   A = [M, K] row-major (K contiguous), B = [N, K] row-major
-//   (the forward x W^T of every nn.Linear: reference model.py:195,215,254,379)
+//   C[M, N] = sum_k A(m, k) * B(k, n)
+//   A: K-contiguous  A(m, k) = a[m * lda + k]   (activations x [T, K]; dY [T, N] of a dX)
+//      k-major (AT)  A(m, k) = a[k * lda + m]   (dY^T of a weight gradient: dY is [T, N], m = n)
+//   B: K-contiguous  B(k, n) = b[n * ldb + k]   (nn.Linear weight [N, K]: every forward)
+//      k-major (BT)  B(k, n) = b[k * ldb + n]   (weight [N, K] read as K x N in dX; X [T, K] in dW)
+// so every product of the transformer step reads its operands as they are stored (reference
+// model.py:195,215,254,379 forward; their dX = dY W and dW = dY^T X backward): no transposed
+// copies, no separate transpose kernel.
 //
 // Structure (one workgroup = one 256 x BN output tile, BN = 32 * NJ, BK = 64):
 //   * 4 waves, one per SIMD, each owning a 128 x (16 NJ) quadrant = 8 x NJ fragments of
@@ -9,18 +15,26 @@
 //     "+a" operands, so the compiler never shuffles them), the operand fragments in VGPRs.
 //     NJ is chosen per shape so the tile count fills the 256 CUs in whole rounds (the 8B step:
 //     qkv 256 x 192 -> 256 tiles, w13 256 x 224 -> 4 x 256, wo / w2 256 x 128 -> 256, head 256^2).
-//   * Both operands are staged by LDS-DMA (buffer_load_dwordx4 ... lds: 1 KiB = 8 rows x 128 B per
-//     wave-instruction, no staging VGPRs; the per-lane source offset XOR-swizzled so the
-//     ds_read_b128 fragment reads are bank-conflict free: chunk c of row r sits at c ^ (r & 7)),
-//     double-buffered (2 stages of 32 + 4 NJ KiB).
+//   * Both operands are staged by LDS-DMA (buffer_load_dwordx4 ... lds: 1 KiB per wave-instruction,
+//     no staging VGPRs, the per-lane SOURCE offset carries the swizzle), double-buffered (2 stages
+//     of 32 + 4 NJ KiB). Two image kinds:
+//       K-contiguous: [rows][64 k], 128-B rows, 16-B chunk c of row r at c ^ (r & 7): the
+//         fragment is one ds_read_b128 (8 consecutive k of one row), conflict-free.
+//       k-major: [64 k][cols], rows of 2 x cols bytes, read with ds_read_b64_tr_b16 (the hardware
+//         transpose: a 16-lane group gets 4 k-rows x 16 columns column-major, so two reads give the
+//         same 8-consecutive-k fragment as ds_read_b128 — the two kinds mix freely). The 32-B
+//         column pair j of k-row k sits at pair j ^ sigma(k), sigma chosen per row length so the
+//         8 rows one 32-lane half reads (k .. k+3, k+8 .. k+11) hit 8 distinct 8-bank windows
+//         (conflict-free); sigma depends on k only through bits the k-step / hi-half offsets never
+//         change, so each fragment needs ONE lane address and the rest are immediates.
 //   * One K-tile = 2 x 8 NJ MFMAs per wave (two k-steps of 32). The fragment registers are
 //     double-buffered by k-step, so every LDS read is issued right behind an MFMA and consumed a
 //     k-step later:
-//       MFMA 0 .. R-1 : the k-step-1 fragment reads of this tile (R = 8 + NJ ds_read_b128)
-//       MFMA 24       : lgkmcnt(0) + barrier  -> every wave has finished reading this stage
-//       then          : the 8 + NJ LDS-DMAs of tile t+2 into this stage, spread evenly
-//       MFMA SB2      : vmcnt(8 + NJ) + barrier -> tile t+1 (issued one K-tile ago) has landed
-//       then          : the k-step-0 fragment reads of tile t+1
+//       MFMA 0 .. RS-1 : the k-step-1 fragment reads of this tile (R read instructions, RPS per MFMA)
+//       MFMA SB1       : lgkmcnt(0) + barrier  -> every wave has finished reading this stage
+//       then           : the 8 + NJ LDS-DMAs of tile t+2 into this stage, spread evenly
+//       MFMA SB2       : vmcnt(8 + NJ) + barrier -> tile t+1 (issued one K-tile ago) has landed
+//       then           : the k-step-0 fragment reads of tile t+1
 //     This is the counts-and-placement schedule of the vendor's tuned assembly GEMMs on this chip
 //     (one wave per SIMD, direct-to-LDS, prefetch two tiles ahead), with HIP choosing registers.
 //   * Epilogue through LDS: per-lane stores straight from the MFMA accumulator layout write 16
@@ -28,10 +42,13 @@
 //     profiles/r3_gemm_w4_investigation.md); each wave instead parks its quadrant in 32 KiB of the
 //     idle LDS (256-B rows, 16-B chunks XOR-swizzled by row: conflict-free 8-B writes and 16-B
 //     row reads) and stores whole rows, 4 x 256 B per instruction. Fused epilogues act on the
-//     row-contiguous values: + residual (wo / w2 into the residual stream), RoPE on the packed
-//     Q/K columns of the QKV projection (reference model.py:100-126: interleaved pairs, fp32).
-//   * Tiles are mapped XCD-contiguously (blockIdx % 8 = XCD under round-robin dispatch),
-//     M-fastest inside an XCD's range, so the XCD's L2 serves the shared B panel.
+//     row-contiguous values: + residual / accumulate (wo / w2 into the residual stream, gradient
+//     accumulation), RoPE on the packed Q/K columns of the QKV projection (reference
+//     model.py:100-126), SwiGLU forward (model.py:254) and backward (dX of w2 -> dgu from the
+//     saved gu), and the per-tile sum of squares of a weight gradient (clip_grad_norm_'s
+//     input, reference utils.py:58-63) so no separate pass re-reads the gradient.
+//   * Tiles are mapped XCD-contiguously (blockIdx % 8 = XCD under round-robin dispatch), rastered
+//     so that the larger operand's panels stay inside one XCD's L2 (M-fastest when B is larger).
 #include "torch_utils.h"
 
 #include <utility>
@@ -51,10 +68,11 @@ __device__ __forceinline__ void sfor(F&& f) {
 
 constexpr int BM = 256, BK = 64, NT = 256;
 constexpr int PIECE = 1024;  // one LDS-DMA wave-instruction: 8 image rows of 128 B
-constexpr int FS = 2 * PIECE;  // one 16-row fragment
-constexpr int OPA = 32 * PIECE;  // A image: 256 rows
+constexpr int FS = 2 * PIECE;  // one 16-row fragment (K-contiguous image)
+constexpr int OPA = 32 * PIECE;  // A image: 256 rows x 64 k
+constexpr int RBA = 2 * BM;      // k-major A image: 512-B k-rows
 
-enum W4Epi : int { W4_STORE = 0, W4_RES = 1, W4_ROPE = 2, W4_SWIGLU = 3 };
+enum W4Epi : int { W4_STORE = 0, W4_RES = 1, W4_ROPE = 2, W4_SWIGLU = 3, W4_SWIGLU_BWD = 4 };
 
 __device__ __forceinline__ unsigned lds_u32(const void* p) {
   return (unsigned)(uintptr_t)((const __attribute__((address_space(3))) char*)p);
@@ -87,6 +105,11 @@ __device__ __forceinline__ void ds16(bf16x8_t& d, unsigned addr) {
   asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(d) : "v"(addr), "i"(OFF) : "memory");
 }
 
+template <int OFF>
+__device__ __forceinline__ void dstr(bf16x4_t& d, unsigned addr) {
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(d) : "v"(addr), "i"(OFF) : "memory");
+}
+
 // bf16 or fp16 operands (--model-dtype): same shape, same schedule, another opcode
 template <class E>
 __device__ __forceinline__ void mfma(f32x4_t& c, const bf16x8_t& a, const bf16x8_t& b) {
@@ -98,7 +121,7 @@ __device__ __forceinline__ void mfma(f32x4_t& c, const bf16x8_t& a, const bf16x8
 
 template <int N>
 __device__ __forceinline__ void lgkm() {
-  asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(N) : "memory");
+  asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(N < 15 ? N : 15) : "memory");
 }
 template <int N>
 __device__ __forceinline__ void vmcnt() {
@@ -106,104 +129,185 @@ __device__ __forceinline__ void vmcnt() {
 }
 __device__ __forceinline__ void barrier() { asm volatile("s_barrier" ::: "memory"); }
 
+// ---- fragments: one 128-bit register (ds_read_b128) or two 64-bit halves (two tr reads) ------
+template <bool T>
+struct Frag;
+template <>
+struct Frag<false> {
+  bf16x8_t v;
+};
+template <>
+struct Frag<true> {
+  bf16x4_t lo, hi;
+};
+__device__ __forceinline__ bf16x8_t val(const Frag<false>& f) { return f.v; }
+__device__ __forceinline__ bf16x8_t val(const Frag<true>& f) {
+  return __builtin_shufflevector(f.lo, f.hi, 0, 1, 2, 3, 4, 5, 6, 7);
+}
 // the registers an asm wait covered: consumers stay behind the wait
-__device__ __forceinline__ void tie(bf16x8_t& x) { asm volatile("" : "+v"(x)); }
+__device__ __forceinline__ void tie(Frag<false>& x) { asm volatile("" : "+v"(x.v)); }
+__device__ __forceinline__ void tie(Frag<true>& x) {
+  asm volatile("" : "+v"(x.lo));
+  asm volatile("" : "+v"(x.hi));
+}
+
+// XOR applied to the 32-B column-pair index of k-row k in a k-major image with RB-byte rows.
+// A 32-lane half of a transposed read takes rows k0 + {0..3, 8..11} (4 lanes x 8 B = one pair per
+// row): they must land in 8 distinct 8-dword bank windows. Row r's pair p is window
+// (r * RB / 32 + (p ^ sigma(r))) mod 8.
+template <int RB>
+__device__ __forceinline__ int tsw(int k) {
+  if constexpr (RB % 256 == 0)  // every row starts in window 0: spread rows over all 8
+    return (k & 3) | (((k >> 3) & 1) << 2);
+  else if constexpr (RB == 448)  // rows 0..3 -> windows 0, 6, 4, 2 already; 8..11 onto the odd ones
+    return (k >> 3) & 1;
+  else if constexpr (RB == 384)  // rows alternate windows 0 / 4: pairs ^ 0..3 fill the rest
+    return ((k >> 1) & 1) | (((k >> 3) & 1) << 1);
+  else
+    static_assert(RB % 256 == 0 || RB == 448 || RB == 384, "k-major image row length");
+  return 0;
+}
 
 struct W4Args {
   const bf16_t* a;
   const bf16_t* b;
   bf16_t* c;
-  const bf16_t* r;       // residual (may alias c) or null
+  const bf16_t* r;       // residual (may alias c: accumulate) or null; W4_SWIGLU_BWD: gu
   const float* cos_t;    // RoPE: [S, D/2] tables
   const float* sin_t;
+  float* part;           // per-tile sums of squares of the stored C (null: none)
   long lda, ldb, ldc, ldr;
   int M, N, K;
   int tiles_m, tiles_n;
+  int nfast;             // raster N-fastest inside an XCD's range (A is the larger operand)
   int rope_cols;         // RoPE: columns [0, rope_cols) are rotated (Hq + Hkv heads)
   int rope_hd;           // head dim
   int rope_seq;          // sequence length (position = row % seq)
   // SwiGLU epilogue (W4_SWIGLU): b = [w1; w3] ([2F, K]); tile tn covers features
   // [tn * 16 NJ, +16 NJ) of BOTH halves (B image rows = that slice of w1, then of w3), so the
   // tile holds g and u of the same features: c = gu [M, 2F], a = silu(g) u [M, F], a^T [F, M]
+  // W4_SWIGLU_BWD: the tile is da [M, F] (dX of w2); c = dgu [M, 2F] from r = gu [M, 2F]
   int ffn;               // F
   bf16_t* act;           // a
-  bf16_t* actT;          // a^T
+  bf16_t* actT;          // a^T (null: not written)
   int exact;             // IEEE division in the sigmoid (FT_EXACT_MATH), as swiglu_fwd_t
 };
 
-__device__ __forceinline__ void tile_of(int bid, int tiles_m, int tiles_n, int& tm, int& tn) {
+// (tm, tn) of workgroup bid (returned by value: through references the pair went to scratch)
+__device__ __forceinline__ int2 tile_of(int bid, int tiles_m, int tiles_n, int nfast) {
   const int nwg = tiles_m * tiles_n;
   const int q = nwg / 8, rem = nwg % 8;
   const int x = bid % 8, o = bid / 8;
   const int w = (x < rem ? x * (q + 1) : rem * (q + 1) + (x - rem) * q) + o;
-  tm = w % tiles_m;
-  tn = w / tiles_m;
+  return nfast ? make_int2(w / tiles_n, w % tiles_n) : make_int2(w % tiles_m, w / tiles_m);
 }
 
-template <int NJ>
+template <int NJ, bool AT, bool BT>
 struct Frags {
-  bf16x8_t a0[8], b0[NJ], a1[8], b1[NJ];
+  Frag<AT> a0[8], a1[8];
+  Frag<BT> b0[NJ], b1[NJ];
 };
 
-template <int NJ>
+template <int NJ, bool AT, bool BT>
 struct Sched {
   static constexpr int MH = 8 * NJ;          // MFMAs per k-step
-  static constexpr int R = 8 + NJ;           // fragment reads per k-step: b[0], a[0..7], b[1..]
+  static constexpr int NA = AT ? 2 : 1;      // read instructions per A / B fragment
+  static constexpr int NB = BT ? 2 : 1;
+  static constexpr int R = 8 * NA + NJ * NB; // read instructions per k-step: b[0], a[0..7], b[1..]
+  static constexpr int F1 = NB + 8 * NA;     // ... of which the first MFMA run needs these
   static constexpr int D = 8 + NJ;           // LDS-DMAs per wave per K-tile (A 8, B NJ)
-  static constexpr int SB1 = 24;             // first barrier (after MFMA 24)
-  static constexpr int SB2 = 2 * MH - R - 4; // second barrier
+  static constexpr int RB = 64 * NJ;         // k-major B image row bytes
+  static constexpr int fits(int rps) {
+    return (2 * MH - (R + rps - 1) / rps - 4) - ((R + rps - 1) / rps + 8 > 24 ? (R + rps - 1) / rps + 8 : 24) - 4 >= D;
+  }
+  static constexpr int RPS = fits(1) ? 1 : 2;  // read instructions per MFMA slot
+  static constexpr int RS = (R + RPS - 1) / RPS;  // MFMA slots the reads of one k-step take
+  static constexpr int SB1 = RS + 8 > 24 ? RS + 8 : 24;  // first barrier (after MFMA SB1)
+  static constexpr int SB2 = 2 * MH - RS - 4;  // second barrier
   static constexpr int dma_slot(int d) { return SB1 + 2 + d * (SB2 - SB1 - 4) / D; }
   static constexpr int OPB = NJ * 4 * PIECE;  // B image
   static constexpr int ST = OPA + OPB;        // stage
-  static_assert(R <= 16 && SB2 - SB1 - 4 >= D && SB2 + R < 2 * MH, "schedule does not fit");
+  static_assert(SB2 - SB1 - 4 >= D && SB2 + RS < 2 * MH, "schedule does not fit");
 };
-
-// lane's part of read r (b[0], a[0..7], b[1..NJ-1]) into the fragment arrays
-template <int NJ, int r>
-__device__ __forceinline__ void rd(bf16x8_t (&ax)[8], bf16x8_t (&bx)[NJ], unsigned ab, unsigned bb) {
-  if constexpr (r == 0)
-    ds16<0>(bx[0], bb);
-  else if constexpr (r <= 8)
-    ds16<FS * (r - 1)>(ax[r - 1], ab);
-  else
-    ds16<FS * (r - 8)>(bx[r - 8], bb);
-}
 
 struct Ctx {
   i32x4_t srdA, srdB;
   unsigned voA[8], voB[8];
-  unsigned rdA0, rdA1, rdB0, rdB1;
+  unsigned rdA0, rdA1, rdB0, rdB1;  // K-contiguous images: k-step 0 / 1 lane address
+  unsigned aT[8], bT[8];            // k-major images: lane address of fragment i (k-step 0, lo)
   unsigned lds0;
+  unsigned stepA, stepB;            // bytes one K-tile advances the A / B source
   int wid;
 };
 
+// read instruction r (b[0], a[0..7], b[1..NJ-1]; a k-major fragment is two: lo, hi) of k-step KK
+// from the stage at byte offset `stage`
+template <int NJ, bool AT, bool BT, int KK, int r>
+__device__ __forceinline__ void rd(Frag<AT> (&ax)[8], Frag<BT> (&bx)[NJ], const Ctx& c, unsigned stage) {
+  using S = Sched<NJ, AT, BT>;
+  constexpr int NA = S::NA, NB = S::NB;
+  constexpr bool isA = r >= NB && r < NB + 8 * NA;
+  if constexpr (isA) {
+    constexpr int i = (r - NB) / NA, h = (r - NB) % NA;
+    if constexpr (AT) {
+      if constexpr (h == 0)
+        dstr<KK * 32 * RBA>(ax[i].lo, c.aT[i] + stage);
+      else
+        dstr<KK * 32 * RBA + 4 * RBA>(ax[i].hi, c.aT[i] + stage);
+    } else {
+      ds16<FS * i>(ax[i].v, (KK ? c.rdA1 : c.rdA0) + stage);
+    }
+  } else {
+    constexpr int j = r < NB ? 0 : 1 + (r - NB - 8 * NA) / NB;
+    constexpr int h = r < NB ? r : (r - NB - 8 * NA) % NB;
+    if constexpr (BT) {
+      constexpr int RB = S::RB;
+      if constexpr (h == 0)
+        dstr<KK * 32 * RB>(bx[j].lo, c.bT[j] + stage);
+      else
+        dstr<KK * 32 * RB + 4 * RB>(bx[j].hi, c.bT[j] + stage);
+    } else {
+      ds16<FS * j>(bx[j].v, (KK ? c.rdB1 : c.rdB0) + stage);
+    }
+  }
+}
+
+// the reads of MFMA slot `slot` (RPS instructions) of k-step KK
+template <int NJ, bool AT, bool BT, int KK, int slot>
+__device__ __forceinline__ void rd_slot(Frag<AT> (&ax)[8], Frag<BT> (&bx)[NJ], const Ctx& c, unsigned stage) {
+  using S = Sched<NJ, AT, BT>;
+  sfor<S::RPS>([&](auto QQ) {
+    constexpr int r = slot * S::RPS + QQ;
+    if constexpr (r < S::R) rd<NJ, AT, BT, KK, r>(ax, bx, c, stage);
+  });
+}
+
 // One K-tile t (stage cur = t & 1): DMA: stage tile t + 2 into this stage; NEXT: read tile t + 1's
 // first k-step.
-template <class E, int NJ, bool DMA, bool NEXT>
-__device__ __forceinline__ void ktile(f32x4_t (&acc)[8][NJ], Frags<NJ>& f, int t, const Ctx& c) {
-  using S = Sched<NJ>;
+template <class E, int NJ, bool AT, bool BT, bool DMA, bool NEXT>
+__device__ __forceinline__ void ktile(f32x4_t (&acc)[8][NJ], Frags<NJ, AT, BT>& f, int t, const Ctx& c) {
+  using S = Sched<NJ, AT, BT>;
   const unsigned cur = (unsigned)(t & 1) * S::ST, nxt = (unsigned)((t + 1) & 1) * S::ST;
-  const unsigned a1b = c.rdA1 + cur, b1b = c.rdB1 + cur, a0n = c.rdA0 + nxt, b0n = c.rdB0 + nxt;
-  const unsigned kofs = (unsigned)(t + 2) * (BK * 2);
+  const unsigned kofsA = (unsigned)(t + 2) * c.stepA, kofsB = (unsigned)(t + 2) * c.stepB;
   const unsigned sb = __builtin_amdgcn_readfirstlane(c.lds0 + cur + c.wid * PIECE);
   sfor<2 * S::MH>([&](auto SS) {
     constexpr int s = SS;
     constexpr int i = s & 7, j = (s % S::MH) >> 3;  // runs of 8 MFMAs share the B fragment (SrcA)
-    if constexpr (s == 0) {  // the first run's 9 fragments landed (issued last K-tile)
-      lgkm<S::R - 9>();
+    if constexpr (s == 0) {  // the first run's fragments landed (issued last K-tile)
+      lgkm<S::R - S::F1>();
       tie(f.b0[0]);
       sfor<8>([&](auto I) { tie(f.a0[I]); });
     }
-    if constexpr (s == 8) {  // all of k-step 0 (8 newer reads in flight)
-      lgkm<8>();
+    if constexpr (s == 8) {  // all of k-step 0 (the k-step-1 reads of slots 0..7 in flight)
+      lgkm<8 * S::RPS>();
       sfor<NJ>([&](auto J) { tie(f.b0[J]); });
     }
     if constexpr (s == 2) asm volatile("s_setprio 3" ::: "memory");
     if constexpr (s < S::MH)
-      mfma<E>(acc[i][j], f.b0[j], f.a0[i]);
+      mfma<E>(acc[i][j], val(f.b0[j]), val(f.a0[i]));
     else
-      mfma<E>(acc[i][j], f.b1[j], f.a1[i]);
-    if constexpr (s < S::R) rd<NJ, s>(f.a1, f.b1, a1b, b1b);
+      mfma<E>(acc[i][j], val(f.b1[j]), val(f.a1[i]));
+    if constexpr (s < S::RS) rd_slot<NJ, AT, BT, 1, s>(f.a1, f.b1, c, cur);
     if constexpr (s == S::SB1) {  // this stage fully read by every wave -> it may be restaged
       lgkm<0>();
       sfor<8>([&](auto I) { tie(f.a1[I]); });
@@ -218,9 +322,9 @@ __device__ __forceinline__ void ktile(f32x4_t (&acc)[8][NJ], Frags<NJ>& f, int t
           constexpr int qa = d < 2 * NJ ? d / 2 : NJ + (d - 2 * NJ);
           constexpr bool isA = d < 2 * NJ ? (d % 2 == 0) : true;
           if constexpr (isA)
-            dma16<qa * 4 * PIECE>(c.srdA, c.voA[qa], kofs, sb);
+            dma16<qa * 4 * PIECE>(c.srdA, c.voA[qa], kofsA, sb);
           else
-            dma16<OPA + (d / 2) * 4 * PIECE>(c.srdB, c.voB[d / 2], kofs, sb);
+            dma16<OPA + (d / 2) * 4 * PIECE>(c.srdB, c.voB[d / 2], kofsB, sb);
         }
       });
     }
@@ -232,42 +336,71 @@ __device__ __forceinline__ void ktile(f32x4_t (&acc)[8][NJ], Frags<NJ>& f, int t
         vmcnt<0>();
       barrier();
     }
-    if constexpr (NEXT && s > S::SB2 && s <= S::SB2 + S::R) rd<NJ, s - S::SB2 - 1>(f.a0, f.b0, a0n, b0n);
+    if constexpr (NEXT && s > S::SB2 && s <= S::SB2 + S::RS) rd_slot<NJ, AT, BT, 0, s - S::SB2 - 1>(f.a0, f.b0, c, nxt);
     if constexpr (s == 2 * S::MH - 1) asm volatile("s_setprio 0" ::: "memory");
   });
 }
 
-template <class E, int NJ, int EPI>
+template <class E, int NJ, int EPI, bool AT, bool BT>
 __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(W4Args p) {
-  using S = Sched<NJ>;
+  using S = Sched<NJ, AT, BT>;
   constexpr int LDS = 2 * S::ST > 4 * 32768 ? 2 * S::ST : 4 * 32768;  // stages / epilogue staging
   __shared__ __attribute__((aligned(1024))) char smem[LDS];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid >> 1, wn = wid & 1;
   constexpr int BN = 32 * NJ, NW = 16 * NJ;
-  int tm, tn;
-  tile_of(blockIdx.x, p.tiles_m, p.tiles_n, tm, tn);
+  const int2 tt = tile_of(blockIdx.x, p.tiles_m, p.tiles_n, p.nfast);
+  const int tm = tt.x, tn = tt.y;
   const int m0 = tm * BM, n0 = tn * BN;
   const int f0 = tn * NW;  // W4_SWIGLU: first feature of the tile (NW features of w1 and of w3)
   const int nk = p.K / BK;
 
-  // LDS-DMA sources: instruction q of wave w covers image rows (q * 4 + w) * 8 + (lane >> 3);
-  // lane's 16-B chunk (lane & 7) holds global chunk (lane & 7) ^ (row & 7)
+  // LDS-DMA sources. Instruction q of wave w fills image piece P = q * 4 + w (bytes [P KiB, +1 KiB)),
+  // lane L its 16 B at P KiB + 16 L; the lane's source is the element that image slot holds.
   Ctx c;
   c.wid = wid;
-  c.srdA = make_srd(p.a + (long)m0 * p.lda);
-  c.srdB = make_srd(EPI == W4_SWIGLU ? p.b : p.b + (long)n0 * p.ldb);
-  const int lrow = wid * 8 + (lane >> 3), lch = (lane & 7) ^ (lane >> 3);
-#pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    c.voA[q] = (unsigned)(((q * 32 + lrow) * p.lda + lch * 8) * 2);
-    const int r = q * 32 + lrow;  // B image row
-    const long src = EPI == W4_SWIGLU ? (r < 16 * NJ ? f0 + r : (long)p.ffn + f0 + (r - 16 * NJ)) : r;
-    c.voB[q] = (unsigned)((src * p.ldb + lch * 8) * 2);
-  }
   c.lds0 = __builtin_amdgcn_readfirstlane(lds_u32(smem));
-  // fragment reads: lane reads row r0 + (lane & 15), chunk (kk * 4 + (lane >> 4)) ^ (lane & 7)
+  const int lrow = wid * 8 + (lane >> 3), lch = (lane & 7) ^ (lane >> 3);
+  if constexpr (AT) {
+    // [64 k][256 m], 512-B rows: piece P holds k-rows 2P, 2P + 1
+    c.srdA = make_srd(p.a + m0);
+    c.stepA = (unsigned)(BK * p.lda * 2);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int off = (q * 4 + wid) * PIECE + lane * 16;
+      const int k = off / RBA, cp = (off % RBA) >> 4;
+      const int gc = cp ^ (2 * tsw<RBA>(k));
+      c.voA[q] = (unsigned)(((long)k * p.lda + gc * 8) * 2);
+    }
+  } else {
+    // [256 rows][64 k], 128-B rows: lane's 16-B chunk (lane & 7) holds global chunk (lane & 7) ^ (row & 7)
+    c.srdA = make_srd(p.a + (long)m0 * p.lda);
+    c.stepA = (unsigned)(BK * 2);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) c.voA[q] = (unsigned)(((q * 32 + lrow) * p.lda + lch * 8) * 2);
+  }
+  if constexpr (BT) {
+    c.srdB = make_srd(p.b + n0);
+    c.stepB = (unsigned)(BK * p.ldb * 2);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int off = (q * 4 + wid) * PIECE + lane * 16;
+      const int k = off / S::RB, cp = (off % S::RB) >> 4;
+      const int gc = cp ^ (2 * tsw<S::RB>(k));
+      c.voB[q] = (unsigned)(((long)k * p.ldb + gc * 8) * 2);
+    }
+  } else {
+    c.srdB = make_srd(EPI == W4_SWIGLU ? p.b : p.b + (long)n0 * p.ldb);
+    c.stepB = (unsigned)(BK * 2);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int r = q * 32 + lrow;  // B image row
+      const long src = EPI == W4_SWIGLU ? (r < 16 * NJ ? f0 + r : (long)p.ffn + f0 + (r - 16 * NJ)) : r;
+      c.voB[q] = (unsigned)((src * p.ldb + lch * 8) * 2);
+    }
+  }
+  // fragment reads, K-contiguous: lane reads row r0 + (lane & 15), chunk (kk * 4 + (lane >> 4)) ^ (lane & 7)
   const unsigned lrowb = (unsigned)(((lane & 15) >> 3) * PIECE + (lane & 7) * 128);
   const unsigned lpart0 = lrowb + (unsigned)((((lane >> 4)) ^ (lane & 7)) << 4);
   const unsigned lpart1 = lrowb + (unsigned)(((4 + (lane >> 4)) ^ (lane & 7)) << 4);
@@ -275,13 +408,31 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(W4Args p) {
   c.rdA1 = c.lds0 + wm * 16 * PIECE + lpart1;
   c.rdB0 = c.lds0 + OPA + wn * NJ * 2 * PIECE + lpart0;
   c.rdB1 = c.lds0 + OPA + wn * NJ * 2 * PIECE + lpart1;
+  // fragment reads, k-major: lane 4q + p of 16-lane group g supplies k-row 8 g + q (k-step 0,
+  // lo half), columns 4p .. 4p + 3 of the fragment's 16 (byte 8 p of its 32-B pair)
+  {
+    const int g = lane >> 4, q4 = (lane & 15) >> 2, pp = lane & 3;
+    const int k0 = 8 * g + q4;
+    if constexpr (AT) {
+      const int sg = tsw<RBA>(k0);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        c.aT[i] = c.lds0 + (unsigned)(k0 * RBA + 32 * ((8 * wm + i) ^ sg) + 8 * pp);
+    }
+    if constexpr (BT) {
+      const int sg = tsw<S::RB>(k0);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+        c.bT[j] = c.lds0 + (unsigned)(OPA + k0 * S::RB + 32 * ((wn * NJ + j) ^ sg) + 8 * pp);
+    }
+  }
 
   f32x4_t acc[8][NJ];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
     for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  Frags<NJ> f;
+  Frags<NJ, AT, BT> f;
 
   // prologue: tiles 0 and 1 in flight, then tile 0's k-step-0 fragments
   const unsigned sb0 = __builtin_amdgcn_readfirstlane(c.lds0 + wid * PIECE);
@@ -289,26 +440,26 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(W4Args p) {
   sfor<8>([&](auto Q) { dma16<Q * 4 * PIECE>(c.srdA, c.voA[Q], 0u, sb0); });
   sfor<NJ>([&](auto Q) { dma16<OPA + Q * 4 * PIECE>(c.srdB, c.voB[Q], 0u, sb0); });
   if (nk > 1) {
-    sfor<8>([&](auto Q) { dma16<Q * 4 * PIECE>(c.srdA, c.voA[Q], (unsigned)(BK * 2), sb1); });
-    sfor<NJ>([&](auto Q) { dma16<OPA + Q * 4 * PIECE>(c.srdB, c.voB[Q], (unsigned)(BK * 2), sb1); });
+    sfor<8>([&](auto Q) { dma16<Q * 4 * PIECE>(c.srdA, c.voA[Q], c.stepA, sb1); });
+    sfor<NJ>([&](auto Q) { dma16<OPA + Q * 4 * PIECE>(c.srdB, c.voB[Q], c.stepB, sb1); });
     vmcnt<S::D>();
   } else {
     vmcnt<0>();
   }
   barrier();
-  sfor<S::R>([&](auto RR) { rd<NJ, RR>(f.a0, f.b0, c.rdA0, c.rdB0); });
+  sfor<S::R>([&](auto RR) { rd<NJ, AT, BT, 0, RR>(f.a0, f.b0, c, 0u); });
 
   // the zeroed accumulators are MFMA sources next (VALU write -> MFMA SrcC wait states)
   __builtin_amdgcn_sched_barrier(0);
   asm volatile("s_nop 4" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
   int t = 0;
-  for (; t + 2 < nk; ++t) ktile<E, NJ, true, true>(acc, f, t, c);
+  for (; t + 2 < nk; ++t) ktile<E, NJ, AT, BT, true, true>(acc, f, t, c);
   if (nk >= 2) {
-    ktile<E, NJ, false, true>(acc, f, t, c);
+    ktile<E, NJ, AT, BT, false, true>(acc, f, t, c);
     ++t;
   }
-  ktile<E, NJ, false, false>(acc, f, t, c);
+  ktile<E, NJ, AT, BT, false, false>(acc, f, t, c);
   // The accumulators are read by VALU next: wait out the last MFMAs (the compiler does not see
   // the asm as MFMAs, so it inserts no wait states), and keep every accumulator read behind the
   // pad (sched_barrier: register-only instructions may otherwise be hoisted above an asm).
@@ -338,6 +489,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(W4Args p) {
   __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes landed
   __builtin_amdgcn_wave_barrier();
   const int cc = lane & 15;
+  float sq = 0.f;  // sum of squares of the stored values (p.part)
   if (cc < 2 * NJ) {
 #pragma unroll 4
     for (int rr = 0; rr < 32; ++rr) {
@@ -346,6 +498,19 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(W4Args p) {
       const long gm = m0 + wm * 128 + row;
       // W4_SWIGLU: wave column half 0 holds g (gu columns [0, F)), half 1 holds u ([F, 2F))
       const int gn = EPI == W4_SWIGLU ? (wn ? p.ffn : 0) + f0 + cc * 8 : n0 + wn * NW + cc * 8;
+      if constexpr (EPI == W4_SWIGLU_BWD) {
+        // v = da (bf16, as the unfused path's GEMM output) for features gn .. gn + 7 of token gm:
+        // dg, du from the saved g = gu[gm, gn], u = gu[gm, F + gn] (swiglu.hip swiglu_grad)
+        float d8[8], g8[8], u8[8], dg[8], du[8];
+        unpack8e<E>(v, d8);
+        unpack8e<E>(*reinterpret_cast<const uint4*>(p.r + gm * p.ldr + gn), g8);
+        unpack8e<E>(*reinterpret_cast<const uint4*>(p.r + gm * p.ldr + p.ffn + gn), u8);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) swiglu_grad(g8[q], u8[q], d8[q], p.exact, dg[q], du[q]);
+        *reinterpret_cast<uint4*>(p.c + gm * p.ldc + gn) = pack8e<E>(dg);
+        *reinterpret_cast<uint4*>(p.c + gm * p.ldc + p.ffn + gn) = pack8e<E>(du);
+        continue;
+      }
       if constexpr (EPI == W4_RES) {
         float a[8], r[8];
         unpack8e<E>(v, a);
@@ -375,8 +540,22 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(W4Args p) {
           v = pack8e<E>(o);
         }
       }
+      if (p.part != nullptr) {
+        float a[8];
+        unpack8e<E>(v, a);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) sq = fmaf(a[q], a[q], sq);
+      }
       *reinterpret_cast<uint4*>(p.c + gm * p.ldc + gn) = v;
     }
+  }
+  if (p.part != nullptr) {  // uniform: one partial per tile, fixed order (deterministic)
+    sq = wave_sum(sq);
+    __syncthreads();  // every wave is done with its staging quadrant
+    float* red = reinterpret_cast<float*>(smem);
+    if (lane == 0) red[wid] = sq;
+    __syncthreads();
+    if (tid == 0) p.part[tn * p.tiles_m + tm] = (red[0] + red[1]) + (red[2] + red[3]);
   }
   if constexpr (EPI == W4_SWIGLU) {
     // a = silu(g) * u from the parked bf16 g / u quadrants (the values just stored to gu, so a is
@@ -400,6 +579,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(W4Args p) {
         *reinterpret_cast<uint4*>(gl + off) = av;
       }
     }
+    if (p.actT == nullptr) return;  // uniform
     __syncthreads();
     // a^T [F, M]: a thread takes 8 tokens x 8 features (8 row-chunk LDS reads, feature chunk
     // fastest across lanes: distinct XOR-swizzled chunks, conflict-free), transposes the block in
@@ -434,28 +614,54 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(W4Args p) {
   }
 }
 
-template <class E, int NJ>
+template <class E, int NJ, bool AT, bool BT>
 void launch_nj(const W4Args& p, int epi, hipStream_t st) {
   const dim3 g(p.tiles_m * p.tiles_n);
+  if constexpr (!AT && !BT) {
+    if (epi == W4_ROPE) {
+      hipLaunchKernelGGL((gemm_w4_kernel<E, NJ, W4_ROPE, false, false>), g, dim3(NT), 0, st, p);
+      return;
+    }
+    if (epi == W4_SWIGLU) {
+      hipLaunchKernelGGL((gemm_w4_kernel<E, NJ, W4_SWIGLU, false, false>), g, dim3(NT), 0, st, p);
+      return;
+    }
+  }
+  if constexpr (!AT && BT) {
+    if (epi == W4_SWIGLU_BWD) {
+      hipLaunchKernelGGL((gemm_w4_kernel<E, NJ, W4_SWIGLU_BWD, false, true>), g, dim3(NT), 0, st, p);
+      return;
+    }
+  }
+  TORCH_CHECK(epi == W4_STORE || epi == W4_RES, "gemm_w4: epilogue ", epi, " not built for this layout");
   if (epi == W4_RES)
-    hipLaunchKernelGGL((gemm_w4_kernel<E, NJ, W4_RES>), g, dim3(NT), 0, st, p);
-  else if (epi == W4_ROPE)
-    hipLaunchKernelGGL((gemm_w4_kernel<E, NJ, W4_ROPE>), g, dim3(NT), 0, st, p);
-  else if (epi == W4_SWIGLU)
-    hipLaunchKernelGGL((gemm_w4_kernel<E, NJ, W4_SWIGLU>), g, dim3(NT), 0, st, p);
+    hipLaunchKernelGGL((gemm_w4_kernel<E, NJ, W4_RES, AT, BT>), g, dim3(NT), 0, st, p);
   else
-    hipLaunchKernelGGL((gemm_w4_kernel<E, NJ, W4_STORE>), g, dim3(NT), 0, st, p);
+    hipLaunchKernelGGL((gemm_w4_kernel<E, NJ, W4_STORE, AT, BT>), g, dim3(NT), 0, st, p);
 }
 
-void launch(at::ScalarType st_, int nj, const W4Args& p, int epi, hipStream_t st) {
+template <bool AT, bool BT>
+void launch_l(at::ScalarType st_, int nj, const W4Args& p, int epi, hipStream_t st) {
   FT_DISPATCH_E16(st_, {
     switch (nj) {
-      case 8: launch_nj<E, 8>(p, epi, st); break;
-      case 7: launch_nj<E, 7>(p, epi, st); break;
-      case 6: launch_nj<E, 6>(p, epi, st); break;
-      default: launch_nj<E, 4>(p, epi, st); break;
+      case 8: launch_nj<E, 8, AT, BT>(p, epi, st); break;
+      case 7: launch_nj<E, 7, AT, BT>(p, epi, st); break;
+      case 6: launch_nj<E, 6, AT, BT>(p, epi, st); break;
+      default: launch_nj<E, 4, AT, BT>(p, epi, st); break;
     }
   });
+}
+
+void launch(at::ScalarType st_, int nj, const W4Args& p, int epi, hipStream_t st, bool at_ = false,
+            bool bt = false) {
+  // the step's layouts: forward (K-contiguous both), dX (k-major B), dW (k-major both)
+  TORCH_CHECK(!at_ || bt, "gemm_w4: k-major A needs a k-major B (the dW layout)");
+  if (at_)
+    launch_l<true, true>(st_, nj, p, epi, st);
+  else if (bt)
+    launch_l<false, true>(st_, nj, p, epi, st);
+  else
+    launch_l<false, false>(st_, nj, p, epi, st);
 }
 
 // Tile width for N: whole rounds of 256 tiles where possible (M = 2048 -> 8 row tiles).
@@ -481,7 +687,7 @@ int pick_nj(long M, long N) {
 
 }  // namespace
 
-// C = A @ B^T (+ residual / RoPE): A [M, K], B [N, K] bf16 row-major; M % 256, K % 64,
+// C = A @ B^T (+ residual): A [M, K], B [N, K] bf16 row-major; M % 256, K % 64,
 // N % (32 * nj) for a tile width in {256, 224, 192, 128}. nj = 0 picks the width per shape.
 at::Tensor gemm_nt_w4(const at::Tensor& a, const at::Tensor& b, const std::optional<at::Tensor>& out,
                       const std::optional<at::Tensor>& residual, int64_t nj) {
@@ -533,6 +739,66 @@ at::Tensor gemm_nt_w4(const at::Tensor& a, const at::Tensor& b, const std::optio
   return c;
 }
 
+// General layouts on the w4 kernel: C[M, N] (=, +=) op(A) op(B), every operand read as stored.
+//   a_t = false: A is [M, K] (lda = K);  a_t = true: A is given as A^T, stored [K, M] (lda = M)
+//   b_t = false: B is [N, K] (ldb = K);  b_t = true: B is stored [K, N] (ldb = N)
+// dX = dY W: gemm_w4_ex(dY [T, N], false, W [N, K], true, T, K, N)
+// dW = dY^T X: gemm_w4_ex(dY [T, N], true, X [T, K], true, N, K, T) (into the flat gradient
+// buffer, accumulate for gradient accumulation, part: the per-tile sums of squares for the
+// gradient norm, tiles_m * tiles_n floats written at part[tn * tiles_m + tm]).
+at::Tensor gemm_w4_ex(const at::Tensor& a, bool a_t, const at::Tensor& b, bool b_t, int64_t M, int64_t N,
+                      int64_t K, const std::optional<at::Tensor>& out, bool accumulate,
+                      const std::optional<at::Tensor>& part, int64_t nj) {
+  FT_CHECK_CUDA(a);
+  TORCH_CHECK(a.scalar_type() == at::kBFloat16 || a.scalar_type() == at::kHalf, "gemm_w4_ex: bf16 / fp16");
+  TORCH_CHECK(b.scalar_type() == a.scalar_type(), "gemm_w4_ex: A / B dtype mismatch");
+  FT_CHECK_CONTIG(a);
+  FT_CHECK_CONTIG(b);
+  TORCH_CHECK(a.numel() == M * K && b.numel() == N * K, "gemm_w4_ex: operand sizes do not match M, N, K");
+  const int NJ = nj > 0 ? (int)nj : pick_nj(M, N);
+  TORCH_CHECK(NJ == 8 || NJ == 7 || NJ == 6 || NJ == 4, "gemm_w4_ex: no tile width fits N = ", N);
+  TORCH_CHECK(M % BM == 0 && N % (32 * NJ) == 0 && K % BK == 0 && K >= BK, "gemm_w4_ex: M % 256, N % ",
+              32 * NJ, ", K % 64 (got ", M, " ", N, " ", K, ")");
+  // 32-bit buffer offsets: the whole operand (a K-tile advance is a scalar offset) under 4 GiB
+  TORCH_CHECK(M * K * 2 < (1L << 32) && N * K * 2 < (1L << 32), "gemm_w4_ex: operand over 4 GiB");
+  const at::DeviceGuard guard(a.device());
+  at::Tensor c;
+  if (out.has_value() && out->defined()) {
+    c = *out;
+    TORCH_CHECK(c.scalar_type() == a.scalar_type(), "gemm_w4_ex: out dtype");
+    FT_CHECK_CONTIG(c);
+    TORCH_CHECK(c.numel() == M * N, "gemm_w4_ex: out has the wrong size");
+  } else {
+    TORCH_CHECK(!accumulate, "gemm_w4_ex: accumulate needs out");
+    c = at::empty({M, N}, a.options());
+  }
+  W4Args p{};
+  p.a = cptr<bf16_t>(a);
+  p.b = cptr<bf16_t>(b);
+  p.c = mptr<bf16_t>(c);
+  p.r = accumulate ? cptr<bf16_t>(c) : nullptr;
+  p.lda = a_t ? M : K;
+  p.ldb = b_t ? N : K;
+  p.ldc = N;
+  p.ldr = N;
+  p.M = M;
+  p.N = N;
+  p.K = K;
+  p.tiles_m = M / BM;
+  p.tiles_n = N / (32 * NJ);
+  p.nfast = M > N;  // keep the larger operand's panels inside one XCD
+  if (part.has_value() && part->defined()) {
+    FT_CHECK_F32((*part));
+    FT_CHECK_CONTIG((*part));
+    TORCH_CHECK(part->numel() >= (long)p.tiles_m * p.tiles_n, "gemm_w4_ex: part holds ", part->numel(),
+                " partials, need ", (long)p.tiles_m * p.tiles_n);
+    p.part = mptr<float>(*part);
+  }
+  launch(a.scalar_type(), NJ, p, accumulate ? W4_RES : W4_STORE, ft_stream(), a_t, b_t);
+  FT_LAUNCH_CHECK();
+  return c;
+}
+
 // Fused QKV projection + RoPE: qkv = x @ w^T with the first (hq + hkv) * d columns (Q and K heads)
 // rotated in the epilogue (interleaved pairs, cos/sin [S, d/2] fp32 tables; row = b * S + s).
 at::Tensor gemm_qkv_rope_w4(const at::Tensor& x, const at::Tensor& w, const at::Tensor& cos_t,
@@ -578,9 +844,10 @@ at::Tensor gemm_qkv_rope_w4(const at::Tensor& x, const at::Tensor& w, const at::
 
 // Fused w1|w3 projection + SwiGLU (reference model.py:254 silu(w1 x) * w3 x): x [M, K],
 // w13 = [w1; w3] [2F, K] -> (gu [M, 2F] = x w13^T for the backward, a = silu(g) u [M, F],
-// a^T [F, M] for the w2 weight gradient). 224-column tiles: 112 features of w1 and the same 112 of
-// w3; M % 256, F % 112, K % 64.
-std::tuple<at::Tensor, at::Tensor, at::Tensor> gemm_swiglu_w4(const at::Tensor& x, const at::Tensor& w13) {
+// a^T [F, M] for a weight gradient on transposed operands, empty when with_t is false).
+// 224-column tiles: 112 features of w1 and the same 112 of w3; M % 256, F % 112, K % 64.
+std::tuple<at::Tensor, at::Tensor, at::Tensor> gemm_swiglu_w4(const at::Tensor& x, const at::Tensor& w13,
+                                                              bool with_t) {
   FT_CHECK_CUDA(x);
   TORCH_CHECK(x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kHalf, "gemm_swiglu_w4: bf16 / fp16");
   TORCH_CHECK(w13.scalar_type() == x.scalar_type(), "gemm_swiglu_w4: x / w13 dtype mismatch");
@@ -595,7 +862,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> gemm_swiglu_w4(const at::Tensor& 
   const at::DeviceGuard guard(x.device());
   auto gu = at::empty({M, F2}, x.options());
   auto a = at::empty({M, F}, x.options());
-  auto aT = at::empty({F, M}, x.options());
+  auto aT = with_t ? at::empty({F, M}, x.options()) : at::empty({0}, x.options());
   W4Args p{};
   p.a = cptr<bf16_t>(x);
   p.b = cptr<bf16_t>(w13);
@@ -610,11 +877,53 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> gemm_swiglu_w4(const at::Tensor& 
   p.tiles_n = F / NWC;
   p.ffn = (int)F;
   p.act = mptr<bf16_t>(a);
-  p.actT = mptr<bf16_t>(aT);
+  p.actT = with_t ? mptr<bf16_t>(aT) : nullptr;
   p.exact = (int)ft_exact_math();
   launch(x.scalar_type(), NJ, p, W4_SWIGLU, ft_stream());
   FT_LAUNCH_CHECK();
   return {gu, a, aT};
+}
+
+// FFN backward through w2 and the SwiGLU (reference model.py:254): da = dy [M, D] @ w2 [D, F]
+// (w2 read as stored: k-major B), and in the epilogue dgu = [dg | du] from the saved gu [M, 2F]
+// (swiglu_grad, as swiglu_bwd) — the separate SwiGLU-backward pass and da itself never exist.
+at::Tensor gemm_swiglu_bwd_w4(const at::Tensor& dy, const at::Tensor& w2, const at::Tensor& gu, int64_t nj) {
+  FT_CHECK_CUDA(dy);
+  TORCH_CHECK(dy.scalar_type() == at::kBFloat16 || dy.scalar_type() == at::kHalf, "gemm_swiglu_bwd_w4: bf16 / fp16");
+  TORCH_CHECK(w2.scalar_type() == dy.scalar_type() && gu.scalar_type() == dy.scalar_type(),
+              "gemm_swiglu_bwd_w4: dtype mismatch");
+  FT_CHECK_CONTIG(dy);
+  FT_CHECK_CONTIG(w2);
+  FT_CHECK_CONTIG(gu);
+  const long D = w2.size(0), F = w2.size(1), M = dy.numel() / D;
+  TORCH_CHECK(dy.numel() == M * D && gu.numel() == M * 2 * F, "gemm_swiglu_bwd_w4: shape mismatch");
+  const int NJ = nj > 0 ? (int)nj : pick_nj(M, F);
+  TORCH_CHECK(NJ == 8 || NJ == 7 || NJ == 6 || NJ == 4, "gemm_swiglu_bwd_w4: no tile width fits F = ", F);
+  TORCH_CHECK(M % BM == 0 && F % (32 * NJ) == 0 && D % BK == 0, "gemm_swiglu_bwd_w4: M % 256, F % ", 32 * NJ,
+              ", D % 64 (got ", M, " ", F, " ", D, ")");
+  TORCH_CHECK(M * D * 2 < (1L << 32) && D * F * 2 < (1L << 32), "gemm_swiglu_bwd_w4: operand over 4 GiB");
+  const at::DeviceGuard guard(dy.device());
+  auto dgu = at::empty({M, 2 * F}, dy.options());
+  W4Args p{};
+  p.a = cptr<bf16_t>(dy);
+  p.b = cptr<bf16_t>(w2);
+  p.c = mptr<bf16_t>(dgu);
+  p.r = cptr<bf16_t>(gu);
+  p.lda = D;
+  p.ldb = F;
+  p.ldc = 2 * F;
+  p.ldr = 2 * F;
+  p.M = M;
+  p.N = F;
+  p.K = D;
+  p.tiles_m = M / BM;
+  p.tiles_n = F / (32 * NJ);
+  p.nfast = 0;
+  p.ffn = (int)F;
+  p.exact = (int)ft_exact_math();
+  launch(dy.scalar_type(), NJ, p, W4_SWIGLU_BWD, ft_stream(), false, true);
+  FT_LAUNCH_CHECK();
+  return dgu;
 }
 
 int64_t gemm_w4_pick(int64_t M, int64_t N) { return pick_nj(M, N); }
@@ -622,8 +931,13 @@ int64_t gemm_w4_pick(int64_t M, int64_t N) { return pick_nj(M, N); }
 TORCH_LIBRARY_FRAGMENT(ftamd, m) {
   m.def("gemm_nt_w4(Tensor a, Tensor b, Tensor(a!)? out=None, Tensor? residual=None, int nj=0) -> Tensor",
         &gemm_nt_w4);
+  m.def(
+      "gemm_w4_ex(Tensor a, bool a_t, Tensor b, bool b_t, int M, int N, int K, Tensor(a!)? out=None, "
+      "bool accumulate=False, Tensor(b!)? part=None, int nj=0) -> Tensor",
+      &gemm_w4_ex);
   m.def("gemm_qkv_rope_w4(Tensor x, Tensor w, Tensor cos, Tensor sin, int seq, int hq, int hkv, int d) -> Tensor",
         &gemm_qkv_rope_w4);
   m.def("gemm_w4_pick(int M, int N) -> int", &gemm_w4_pick);
-  m.def("gemm_swiglu_w4(Tensor x, Tensor w13) -> (Tensor, Tensor, Tensor)", &gemm_swiglu_w4);
+  m.def("gemm_swiglu_w4(Tensor x, Tensor w13, bool with_t=True) -> (Tensor, Tensor, Tensor)", &gemm_swiglu_w4);
+  m.def("gemm_swiglu_bwd_w4(Tensor dy, Tensor w2, Tensor gu, int nj=0) -> Tensor", &gemm_swiglu_bwd_w4);
 }

@@ -371,10 +371,12 @@ __global__ __launch_bounds__(1024) void norm_bwd_split_kernel(
 // Column sums of a [P, N] fp32 slab -> model-dtype dw (optionally accumulated).
 // Block = 32 columns x 8 row groups (128-B row segments); fixed summation order
 // (deterministic). 128 blocks for N = 4096.
+// sq (optional): block i writes sq[i] = the sum of squares of its 32 stored dw values (the
+// gradient norm's partials, ops/grad_sink.py: no separate pass over the norm weights' gradient).
 template <class E>
 __global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ part,
                                                      typename E::T* __restrict__ dw, int P, int N,
-                                                     bool accumulate) {
+                                                     bool accumulate, float* __restrict__ sq) {
   __shared__ float red[8][33];
   const int cl = threadIdx.x & 31, g = threadIdx.x >> 5;
   const int col = blockIdx.x * 32 + cl;
@@ -385,12 +387,23 @@ __global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ p
   }
   red[g][cl] = s;
   __syncthreads();
-  if (g == 0 && col < N) {
-    float t = 0.f;
+  if (g == 0) {  // lanes 0..31 of wave 0
+    float q = 0.f;
+    if (col < N) {
+      float t = 0.f;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) t += red[k][cl];
-    if (accumulate) t += ld1<E>(dw + col);
-    dw[col] = cvt1<E>(t);
+      for (int k = 0; k < 8; ++k) t += red[k][cl];
+      if (accumulate) t += ld1<E>(dw + col);
+      const typename E::T o = cvt1<E>(t);
+      dw[col] = o;
+      const float f = ld1<E>(&o);
+      q = f * f;
+    }
+    if (sq != nullptr) {
+#pragma unroll
+      for (int o = 16; o > 0; o >>= 1) q += __shfl_xor(q, o, 32);
+      if (cl == 0) sq[blockIdx.x] = q;
+    }
   }
 }
 
@@ -590,7 +603,8 @@ std::tuple<at::Tensor, at::Tensor> norm_bwd_part(const at::Tensor& dy, const at:
 }
 
 // dw ([N], model dtype) = column sums of part [P, N] (+ dw when accumulating); fixed order.
-void colsum_(const at::Tensor& part, const at::Tensor& dw, bool accumulate) {
+// sq: ceil(N / 32) fp32 sums of squares of the stored dw, one per 32 columns (optional).
+void colsum_(const at::Tensor& part, const at::Tensor& dw, bool accumulate, const std::optional<at::Tensor>& sq) {
   FT_CHECK_CUDA(part);
   FT_CHECK_CONTIG(part);
   FT_CHECK_MODEL_DTYPE(dw);
@@ -599,20 +613,27 @@ void colsum_(const at::Tensor& part, const at::Tensor& dw, bool accumulate) {
               "colsum_: part must be fp32 [P, N] with N = dw.numel()");
   const at::DeviceGuard guard(dw.device());
   const int N = dw.numel();
+  float* sqp = nullptr;
+  if (sq.has_value() && sq->defined()) {
+    FT_CHECK_F32((*sq));
+    FT_CHECK_CONTIG((*sq));
+    TORCH_CHECK(sq->numel() >= (N + 31) / 32, "colsum_: sq needs ceil(N / 32) floats");
+    sqp = mptr<float>(*sq);
+  }
   FT_DISPATCH_E(dw.scalar_type(),
                 hipLaunchKernelGGL((colsum_kernel<E>), dim3((N + 31) / 32), dim3(256), 0,
                                    ft_stream(), cptr<float>(part), mptr<typename E::T>(dw),
-                                   (int)part.size(0), N, accumulate));
+                                   (int)part.size(0), N, accumulate, sqp));
   FT_LAUNCH_CHECK();
 }
 
 at::Tensor norm_bwd(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& w,
                     const at::Tensor& rstd, const std::optional<at::Tensor>& mean,
                     const at::Tensor& dw, const std::optional<at::Tensor>& dres,
-                    bool accumulate) {
+                    bool accumulate, const std::optional<at::Tensor>& sq) {
   TORCH_CHECK(dw.numel() == w.numel(), "norm_bwd: dw shape mismatch");
   auto r = norm_bwd_part(dy, x, w, rstd, mean, dres);
-  colsum_(std::get<1>(r), dw, accumulate);
+  colsum_(std::get<1>(r), dw, accumulate, sq);
   return std::get<0>(r);
 }
 
@@ -627,9 +648,9 @@ TORCH_LIBRARY_FRAGMENT(ftamd, m) {
       "norm_bwd_part(Tensor dy, Tensor x, Tensor w, Tensor rstd, Tensor? mean, Tensor? dres) -> "
       "(Tensor, Tensor)",
       &norm_bwd_part);
-  m.def("colsum_(Tensor part, Tensor(a!) dw, bool accumulate) -> ()", &colsum_);
+  m.def("colsum_(Tensor part, Tensor(a!) dw, bool accumulate, Tensor(b!)? sq=None) -> ()", &colsum_);
   m.def(
       "norm_bwd(Tensor dy, Tensor x, Tensor w, Tensor rstd, Tensor? mean, Tensor(a!) dw, "
-      "Tensor? dres, bool accumulate) -> Tensor",
+      "Tensor? dres, bool accumulate, Tensor(b!)? sq=None) -> Tensor",
       &norm_bwd);
 }

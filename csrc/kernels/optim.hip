@@ -245,6 +245,10 @@ void adamw_(const at::Tensor& p, const at::Tensor& g, const at::Tensor& m, const
   // parameter dtype P (= gradient dtype) in {bf16, fp16, fp32}; moments S either P or fp32
   TORCH_CHECK(m.scalar_type() == p.scalar_type() || m.scalar_type() == at::kFloat,
               "adamw: optimizer states must have the parameter dtype or fp32");
+  // fp32 parameters (--model-dtype fp32) always take the IEEE division / square root: the
+  // hardware v_rcp_f32 / v_sqrt_f32 (1 ulp) are below bf16/fp16 storage rounding but not below
+  // fp32's, where torch AdamW's exact math is the parity target (docs/PARITY.md)
+  const int exact = (int)ft_exact_math() || p.scalar_type() == at::kFloat;
   auto go = [&](auto ptag, auto stag) {
     using P = decltype(ptag);
     using S = decltype(stag);
@@ -254,12 +258,12 @@ void adamw_(const at::Tensor& p, const at::Tensor& g, const at::Tensor& m, const
       hipLaunchKernelGGL((adamw_kernel<P, S, true>), grid, block, 0, ft_stream(), mptr<PT>(p),
                          cptr<PT>(g), mptr<ST>(m), mptr<ST>(v), n8, (float)lr, (float)beta1,
                          (float)beta2, (float)eps, (float)wd, inv_bc1, inv_sqrt_bc2,
-                         cptr<float>(stats), hp, (int)ft_exact_math());
+                         cptr<float>(stats), hp, exact);
     else
       hipLaunchKernelGGL((adamw_kernel<P, S, false>), grid, block, 0, ft_stream(), mptr<PT>(p),
                          cptr<PT>(g), mptr<ST>(m), mptr<ST>(v), n8, (float)lr, (float)beta1,
                          (float)beta2, (float)eps, (float)wd, inv_bc1, inv_sqrt_bc2,
-                         cptr<float>(stats), hp, (int)ft_exact_math());
+                         cptr<float>(stats), hp, exact);
   };
   FT_DISPATCH_E(p.scalar_type(), {
     if (m.scalar_type() == at::kFloat) go(E{}, EF32{});

@@ -12,16 +12,6 @@
 namespace {
 
 
-// d/dg, d/du of silu(g) * u given the upstream d, with every fma explicit so the element-wise and
-// the tiled kernels round identically (the contraction the compiler picks otherwise differs by
-// kernel once the division is a plain v_rcp_f32).
-__device__ __forceinline__ void swiglu_grad(float g, float u, float d, bool exact, float& dg, float& du) {
-  const float s = sigmoid_f(g, exact);
-  const float silu = g * s;
-  du = d * silu;
-  dg = (d * u) * fmaf(silu, 1.f - s, s);
-}
-
 template <class E>
 __global__ __launch_bounds__(256) void swiglu_fwd_kernel(const typename E::T* __restrict__ gu,
                                                          typename E::T* __restrict__ a, long T, int F, int exact) {

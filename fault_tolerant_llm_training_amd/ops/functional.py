@@ -108,6 +108,9 @@ def set_w4_dw(on: bool) -> None:
 
 
 _W4_DTYPES = (torch.bfloat16, torch.float16)  # bf16 / fp16 MFMA variants of the kernel
+# Output tiles (of 256 rows) a product needs before it goes to the w4 kernel: half the chip.
+# (Tests lower it to drive small shapes through the same paths.)
+_W4_MIN_TILES = 128
 
 
 def _w4_fits(x2: torch.Tensor, w: torch.Tensor, max_nj: int = 8) -> bool:
@@ -119,7 +122,7 @@ def _w4_fits(x2: torch.Tensor, w: torch.Tensor, max_nj: int = 8) -> bool:
     nj = kernels().gemm_w4_pick(T, w.shape[0])
     # at least half the chip in tiles: smaller products (GPT-2-sized, K = 768-1024) are
     # latency-bound and stay on the vendor kernels
-    return 0 < nj <= max_nj and (T // 256) * (w.shape[0] // (32 * nj)) >= 128
+    return 0 < nj <= max_nj and (T // 256) * (w.shape[0] // (32 * nj)) >= _W4_MIN_TILES
 
 
 def _w4_ok(x2: torch.Tensor, w: torch.Tensor) -> bool:
@@ -165,10 +168,43 @@ def mm_fwd(x2: torch.Tensor, w: torch.Tensor, residual: Optional[torch.Tensor] =
     return torch.addmm(residual.reshape(T, N), x2, w.t())
 
 
-def mm_dx(dy2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+# Backward GEMMs on the w4 kernel's k-major layouts (csrc/kernels/gemm_w4.hip, gemm_w4_ex): dX = dY W
+# reads the weight [N, K] as stored, dW = dY^T X reads dY [T, N] and X [T, K] as stored, through
+# ds_read_b64_tr_b16 transposed LDS reads -- no transposed copies, no transpose kernel. The dW
+# epilogue also writes the gradient's per-tile sums of squares into the sink's norm partials (one
+# GPU), so no separate pass re-reads the gradient for clip_grad_norm_. Default on; FT_W4_BWD=0
+# restores the round-3 routing (hipBLASLt, transposed copies for dW) for A/B runs.
+_W4_BWD = os.environ.get("FT_W4_BWD", "1") != "0"
+
+
+def set_w4_bwd(on: bool) -> None:
+    global _W4_BWD
+    _W4_BWD = bool(on)
+
+
+def _w4t_fits(M: int, N: int, K: int, *ts) -> bool:
+    """C[M, N] over a K-deep sum on the w4 kernel: 16-bit CUDA operands of one dtype, a tile width
+    for N, and at least half the chip in tiles (smaller, GPT-2-sized products are latency-bound
+    and stay on the vendor kernels)."""
+    if not (_W4_BWD and _GEMM_MODE != "blas" and all(t.is_cuda and t.dtype in _W4_DTYPES for t in ts)
+            and len({t.dtype for t in ts}) == 1):
+        return False
+    if M % 256 or K % 64 or K < 64:
+        return False
+    nj = kernels().gemm_w4_pick(M, N)
+    return 0 < nj and (M // 256) * (N // (32 * nj)) >= _W4_MIN_TILES
+
+
+def mm_dx(dy2: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """dx = dy2 @ w: dy2 [T, N], w [N, K]."""
     T, N = dy2.shape
     K = w.shape[1]
+    if _w4t_fits(T, K, N, dy2, w) and w.is_contiguous():
+        return kernels().gemm_w4_ex(dy2.contiguous(), False, w, True, T, K, N, out, False, None, 0)
+    if out is not None:
+        if _hand("dx", T, K, N, dy2, w):
+            return kernels().gemm(dy2.contiguous(), True, w, False, T, K, N, out, None, False, 0)
+        return torch.mm(dy2, w, out=out)
     if _hand("dx", T, K, N, dy2, w):
         return kernels().gemm(dy2.contiguous(), True, w, False, T, K, N, None, None, False, 0)
     return torch.mm(dy2, w)
@@ -206,6 +242,15 @@ def weight_grad(dy2: torch.Tensor, x2: torch.Tensor, sink: Optional[GradSink],
         x2 = xT.t()
     T, N = dy2.shape
     K = x2.shape[1]
+    if dyT is None and xT is None and _w4t_fits(N, K, T, dy2, x2) and dy2.is_contiguous() and x2.is_contiguous():
+        # dW[N, K] = dY^T X, both read as stored (k-major A and B), straight into the sink
+        if sink is None:
+            return kernels().gemm_w4_ex(dy2, True, x2, True, N, K, T, None, False, None, 0)
+        kernels().gemm_w4_ex(dy2, True, x2, True, N, K, T, sink.buf.view(N, K), sink.accumulate, sink.part, 0)
+        if sink.part is not None:
+            sink.sq_done = True
+        sink.ready()
+        return None
     if xT is not None and dyT is None and _hand("dw", N, K, T, dy2, xT) and dy2.is_contiguous() \
             and xT.is_contiguous():
         # dW[N, K] = dY^T X with X given transposed (the SwiGLU kernels' a^T [K, T]): the hand
@@ -297,7 +342,8 @@ def weight_grad_async(dy2: torch.Tensor, x2: Optional[torch.Tensor], sink: Optio
     x2 = x2.contiguous() if x2 is not None else None
     xx = x2 if x2 is not None else xT.t()
     bufs = None
-    if _use_tn(dy2, xx) and not _hand("dw", dy2.shape[1], xx.shape[1], dy2.shape[0], dy2, xx):
+    w4t = dyT is None and xT is None and _w4t_fits(dy2.shape[1], xx.shape[1], dy2.shape[0], dy2, xx)
+    if not w4t and _use_tn(dy2, xx) and not _hand("dw", dy2.shape[1], xx.shape[1], dy2.shape[0], dy2, xx):
         T, N = dy2.shape
         bufs = (dy2.new_empty((N, T)) if dyT is None else None,
                 xx.new_empty((xx.shape[1], T)) if xT is None else None)
@@ -332,10 +378,13 @@ def join_dw_stream() -> None:
 
 
 def norm_bwd_into_sink(dy, x, w, rstd, mean, sink: GradSink, dres=None) -> torch.Tensor:
-    """dx of the (add-)norm backward; dW folded into ``sink`` (then ``sink.ready()``).
+    """dx of the (add-)norm backward; dW folded into ``sink`` (then ``sink.ready()``), with its
+    per-column-block sums of squares into the sink's norm partials when it has them.
     (Folding dW on the dW side stream instead was measured at no gain:
     profiles/r1_norm_fold_side_ab.log.)"""
-    dx = kernels().norm_bwd(dy, x, w, rstd, mean, sink.buf, dres, sink.accumulate)
+    dx = kernels().norm_bwd(dy, x, w, rstd, mean, sink.buf, dres, sink.accumulate, sink.part)
+    if sink.part is not None:
+        sink.sq_done = True
     sink.ready()
     return dx
 
@@ -629,6 +678,7 @@ def rope_attention(qkv, cos, sin, seq_len, hq, hkv, d, keep: Optional[AttentionK
 # kernel alone runs the Llama-3-8B QKV shape at 1.10-1.14x hipBLASLt, profiles/r3_gemm_w4_investigation.md);
 # FT_QKV_ROPE=0 restores hipBLASLt + the RoPE kernel.
 _QKV_ROPE = os.environ.get("FT_QKV_ROPE", "1") != "0"
+_QKV_ROPE_MIN_K = 2048  # model dim from which the fused projection wins (see _qkv_rope_ok)
 
 
 def set_qkv_rope(on: bool) -> None:
@@ -637,12 +687,12 @@ def set_qkv_rope(on: bool) -> None:
 
 
 def _qkv_rope_ok(x2: torch.Tensor, w: torch.Tensor, d: int) -> bool:
-    if not (_QKV_ROPE and _GEMM_MODE != "blas" and x2.is_cuda and x2.dtype in _W4_DTYPES
+    if not (_QKV_ROPE and _W4_FWD and _GEMM_MODE != "blas" and x2.is_cuda and x2.dtype in _W4_DTYPES
             and w.dtype == x2.dtype):
         return False
     # K >= 2048 (the 8B-class projections): at GPT-2 sizes (K = 768 / 1024) the epilogue kernel
     # loses ~1 % of the step to hipBLASLt + the RoPE kernel (profiles/r3_gpt2_w4_ab.log)
-    return d % 8 == 0 and x2.shape[1] >= 2048 and _w4_fits(x2, w)
+    return d % 8 == 0 and x2.shape[1] >= _QKV_ROPE_MIN_K and _w4_fits(x2, w)
 
 
 class QKVRopeFn(torch.autograd.Function):
@@ -742,9 +792,59 @@ def _swiglu_w4_ok(x2: torch.Tensor, w13: torch.Tensor) -> bool:
         return False
     T, K = x2.shape
     F = w13.shape[0] // 2
-    if T % 256 or K % 64 or F % 112 or (T // 256) * (F // 112) < 128:
+    if T % 256 or K % 64 or F % 112 or (T // 256) * (F // 112) < _W4_MIN_TILES:
         return False
     return _DW_MODE == "all" or (_DW_MODE != "none" and 2.0 * T * 2 * F * K >= _DW_MIN_FLOP)
+
+
+def _ffn_w4t_ok(x2: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor) -> bool:
+    """Every FFN product on the w4 kernel with no transposed operand anywhere: forward w1|w3 with the
+    SwiGLU epilogue (F % 112), backward da on k-major w2 with the SwiGLU-backward epilogue, dW2 /
+    dW13 on k-major dY and activations, dX on k-major w13 (bf16 or fp16)."""
+    if not (_W4_SWIGLU and _W4_FWD and _W4_BWD and x2.is_cuda and x2.dtype in _W4_DTYPES
+            and w13.dtype == x2.dtype and w2.dtype == x2.dtype):
+        return False
+    T, D = x2.shape
+    F = w2.shape[1]
+    if T % 256 or D % 64 or F % 112 or (T // 256) * (F // 112) < _W4_MIN_TILES:
+        return False
+    return (_w4t_fits(T, F, D, x2, w2) and _w4t_fits(2 * F, D, T, x2) and _w4t_fits(D, F, T, x2)
+            and _w4t_fits(T, D, 2 * F, x2))
+
+
+class FeedForwardW4Fn(torch.autograd.Function):
+    """x -> [w1; w3] GEMM + SwiGLU -> w2 GEMM, every product on the w4 kernel, no transposes:
+
+    forward   (gu, a) = gemm_swiglu_w4(x, w13)     SwiGLU in the epilogue, gu kept for backward
+              y = a w2^T
+    backward  dW2 = dy^T a                          k-major dy and a, sums of squares in the epilogue
+              dgu = gemm_swiglu_bwd_w4(dy, w2, gu)  da = dy w2 (k-major w2), SwiGLU backward in the
+                                                    epilogue: neither da nor a SwiGLU pass exists
+              dW13 = dgu^T x ; dx = dgu w13         k-major dgu / x / w13
+    Reference math: model.py:253-254."""
+
+    @staticmethod
+    def forward(ctx, x, w13, w2, sink13, sink2):
+        K_ = kernels()
+        D = x.shape[-1]
+        x2 = x.reshape(-1, D).contiguous()
+        gu, a, _ = K_.gemm_swiglu_w4(x2, w13, False)
+        y = mm_fwd(a, w2)
+        ctx.sinks = (sink13, sink2)
+        ctx.xshape = x.shape
+        ctx.save_for_backward(x2, gu, a, w13, w2)
+        return y.view(*x.shape[:-1], w2.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, gu, a, w13, w2 = ctx.saved_tensors
+        sink13, sink2 = ctx.sinks
+        dy2 = dy.reshape(-1, w2.shape[0]).contiguous()
+        dw2 = weight_grad_async(dy2, a, sink2)
+        dgu = kernels().gemm_swiglu_bwd_w4(dy2, w2, gu, 0)
+        dw13 = weight_grad_async(dgu, x2, sink13)
+        dx = mm_dx(dgu, w13).view(ctx.xshape)
+        return dx, dw13, dw2, None, None
 
 
 class FeedForwardFn(torch.autograd.Function):
@@ -841,6 +941,8 @@ def feed_forward(x, w13, w2, sink13=None, sink2=None):
     if x.is_cuda and _FUSED_FFN:
         T, D = x.numel() // x.shape[-1], x.shape[-1]
         F = w13.shape[0] // 2
+        if _ffn_w4t_ok(x.reshape(T, D), w13, w2):
+            return FeedForwardW4Fn.apply(x, w13, w2, sink13, sink2)
         # gemm_swiglu / gemm_swiglu_bwd tile T and F by 256 (BM / BN of the 256 kernel)
         if _hand("ffn", T, 2 * F, D, x, w13, w2) and F % 256 == 0 and T % 256 == 0:
             return FusedFFNFn.apply(x, w13, w2, sink13, sink2)
@@ -877,16 +979,27 @@ def _dx_into(out: torch.Tensor, dy2: torch.Tensor, w: torch.Tensor) -> None:
     """out[T, K] = dy2[T, N] @ w[N, K]."""
     T, N = dy2.shape
     K = w.shape[1]
+    if _w4t_fits(T, K, N, dy2, w) and out.is_contiguous() and w.is_contiguous():
+        kernels().gemm_w4_ex(dy2, False, w, True, T, K, N, out, False, None, 0)
+        return
     if _hand("dx", T, K, N, dy2, w):
         kernels().gemm(dy2, True, w, False, T, K, N, out, None, False, 0)
     else:
         torch.mm(dy2, w, out=out)
 
 
-def _dw_into(out: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor, accumulate: bool) -> None:
-    """out[N, K] (+)= dy2[T, N]^T @ x2[T, K]."""
+def _dw_into(out: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor, accumulate: bool,
+             sink: Optional[GradSink] = None) -> None:
+    """out[N, K] (+)= dy2[T, N]^T @ x2[T, K]. ``sink``: the final write of the sink's gradient
+    (its norm partials come from this product's epilogue)."""
     T, N = dy2.shape
     K = x2.shape[1]
+    if _w4t_fits(N, K, T, dy2, x2) and dy2.is_contiguous() and x2.is_contiguous():
+        part = sink.part if sink is not None else None
+        kernels().gemm_w4_ex(dy2, True, x2, True, N, K, T, out, accumulate, part, 0)
+        if part is not None:
+            sink.sq_done = True
+        return
     if _hand("dw", N, K, T, dy2, x2):
         kernels().gemm(dy2, False, x2, False, N, K, T, out, None, accumulate, 0)
         return
@@ -902,6 +1015,23 @@ def _dw_into(out: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor, accumulate:
         out.addmm_(dy2.t(), x2)
     else:
         torch.mm(dy2.t(), x2, out=out)
+
+
+# The head's logits GEMM (h W^T, [T, V]) on the w4 kernel's 256-wide tiles as well (FT_W4_HEAD=0:
+# hipBLASLt). The other forward products use the w4 kernel only up to tile width 6
+# (FT_W4_FWD_MAX_NJ); the head takes the widest tile.
+_W4_HEAD = os.environ.get("FT_W4_HEAD", "1") != "0"
+
+
+def set_w4_head(on: bool) -> None:
+    global _W4_HEAD
+    _W4_HEAD = bool(on)
+
+
+def _head_fwd(h2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    if _W4_HEAD and _W4_FWD and _w4_fits(h2, w) and h2.is_contiguous():
+        return kernels().gemm_nt_w4(h2, w, None, None, 0)
+    return mm_fwd(h2, w)
 
 
 class LMHeadCrossEntropyFn(torch.autograd.Function):
@@ -948,13 +1078,13 @@ class LMHeadCrossEntropyFn(torch.autograd.Function):
         losses, lses = [], []
         for c, r0 in enumerate(range(0, T, rows)):
             hc, lc = h2[r0 : r0 + rows], lab[r0 : r0 + rows]
-            logits = mm_fwd(hc, weight)
+            logits = _head_fwd(hc, weight)
             lr, lse = K_.xent_fwd(logits, lc, IGNORE_INDEX)
             losses.append(lr)
             if fused:
                 K_.xent_bwd_(logits, lc, lse, one, inv, IGNORE_INDEX)  # logits := dlogits
                 _dx_into(dh[r0 : r0 + rows], logits, weight)
-                _dw_into(dw, logits, hc, c > 0)
+                _dw_into(dw, logits, hc, c > 0, sink if r0 + rows >= T else None)
             else:
                 lses.append(lse)
             del logits
@@ -984,6 +1114,8 @@ class LMHeadCrossEntropyFn(torch.autograd.Function):
             K_.scale_by_(dh, gf)
             if sink is not None:
                 K_.scale_by_(sink.buf, gf)
+                if sink.sq_done:  # the epilogue's sums of squares were of the unscaled dW
+                    sink.part.mul_(gf * gf)
                 sink.ready()
                 return dh.view(ctx.hshape), None, None, None, None
             K_.scale_by_(dw, gf)
@@ -997,10 +1129,10 @@ class LMHeadCrossEntropyFn(torch.autograd.Function):
         acc0 = sink.accumulate if sink is not None else False
         for c, r0 in enumerate(range(0, T, rows)):
             hc, lc = h2[r0 : r0 + rows], lab[r0 : r0 + rows]
-            logits = mm_fwd(hc, w)
+            logits = _head_fwd(hc, w)
             K_.xent_bwd_(logits, lc, lse[r0 : r0 + rows].contiguous(), gf, inv, IGNORE_INDEX)
             _dx_into(dh[r0 : r0 + rows], logits, w)
-            _dw_into(dw, logits, hc, acc0 or c > 0)
+            _dw_into(dw, logits, hc, acc0 or c > 0, sink if r0 + rows >= T else None)
             del logits
         if sink is not None:
             sink.ready()

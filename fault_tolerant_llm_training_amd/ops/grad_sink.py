@@ -15,7 +15,7 @@ import torch
 
 
 class GradSink:
-    __slots__ = ("buf", "start", "end", "accumulate", "hook", "name", "gather", "defer", "stash")
+    __slots__ = ("buf", "start", "end", "accumulate", "hook", "name", "gather", "defer", "stash", "part", "sq_done")
 
     def __init__(self, buf: torch.Tensor, start: int = 0, end: int = 0, name: str = ""):
         self.buf = buf
@@ -30,6 +30,12 @@ class GradSink:
         # stashed here (defer=True) and exchanged together in the last micro-batch
         self.defer = False
         self.stash: list = []
+        # gradient-norm partials (one GPU, parallel.ddp.GradReducer "local" mode): a slice of the
+        # reducer's partial sums of squares that the producing kernel fills in its epilogue (the
+        # w4 dW GEMM per output tile, the norm backward per column block); it then sets sq_done
+        # and the reducer skips the separate sum-of-squares pass over this gradient
+        self.part: Optional[torch.Tensor] = None
+        self.sq_done = False
 
     def ready(self) -> None:
         if self.hook is not None:

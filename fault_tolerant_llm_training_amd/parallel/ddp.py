@@ -73,6 +73,43 @@ def set_sumsq_at_end(on: bool) -> None:
     SUMSQ_AT_END = bool(on)
 
 
+# One GPU ("local" mode): the gradient norm's partial sums of squares come from the kernels that
+# write the gradients (the w4 dW GEMM's epilogue per output tile, the norm backward's column sums
+# per 32 columns) into a per-sink slice of ``partials``; only gradients whose producer has no such
+# epilogue (the embedding's scatter-add, hipBLASLt fallbacks) get the separate sumsq pass. The
+# 16 GB re-read of the Llama-3-8B gradient per step is gone. FT_FUSED_SUMSQ=0: per-bucket passes.
+# (Under DP the norm is of the REDUCED gradient, so the passes run after each bucket's collective.)
+FUSED_SUMSQ = os.environ.get("FT_FUSED_SUMSQ", "1") == "1"
+
+
+def set_fused_sumsq(on: bool) -> None:
+    global FUSED_SUMSQ
+    FUSED_SUMSQ = bool(on)
+
+
+def sink_partials(numel: int, ndim: int) -> int:
+    """Partial slots a sink's producers may write: one per w4 output tile (>= 256 x 128 elements)
+    of a 2-D weight, one per 32 columns of a 1-D one; also the grid of the fallback sumsq pass."""
+    if ndim <= 1:
+        return max(1, (numel + 31) // 32)
+    return max(1, (numel + 32767) // 32768)
+
+
+def _copy_back(dst: torch.Tensor, src: torch.Tensor, temps) -> None:
+    """fp32 reduce: round the reduced fp32 copy back into the gradient buffer.
+
+    Runs on the stream that waited for the collective (the reducer's side stream), while the
+    fp32 temporaries were allocated on the stream that launched the bucket (compute or dW
+    stream). Their last Python references are dropped right after this enqueue, so they are
+    recorded on the current stream: the caching allocator then keeps their blocks until this
+    copy has read them, instead of handing them to the next bucket's ``grads.float()``."""
+    dst.copy_(src)
+    if src.is_cuda:
+        cur = torch.cuda.current_stream(src.device)
+        for t in temps:
+            t.record_stream(cur)
+
+
 class Bucket:
     __slots__ = ("idx", "lo", "hi", "needed", "filled", "launched", "work", "part_lo", "part_hi",
                  "shard_lo", "shard_len", "event", "sparse", "post")
@@ -147,7 +184,6 @@ class GradReducer:
             mode = "allreduce"  # shards must stay 8-element aligned for the vector kernels
         self.mode = mode
         self.cuda = flat.device.type == "cuda"
-        self.overlap = self.cuda if overlap is None else (overlap and self.cuda)
         # Sparse embedding exchange (DP): the token-embedding gradient has at most B*S nonzero
         # rows per rank (2048 of 131072 for Llama-3-8B), yet reducing it densely moves 1 GB per
         # step at the very end of backward, right on the critical path into the next forward.
@@ -168,14 +204,39 @@ class GradReducer:
                 if b.lo == es.offset and b.hi == es.offset + es.numel:
                     b.sparse = True
             flat.sinks[emb].gather = self._gather_rows
-        # partial sums of squares: a fixed slice per bucket -> deterministic total
+        self.overlap = self.cuda if overlap is None else (overlap and self.cuda)
+        # partial sums of squares: a fixed slice per bucket (or per sink, FUSED_SUMSQ) -> the
+        # total is a fixed-order sum, deterministic
+        self.fused_sumsq = FUSED_SUMSQ and mode == "local" and self.cuda and self.overlap
+        self._sq_sinks: List[GradSink] = []
+        self._bucket_sq_sinks: List[List[GradSink]] = [[] for _ in self.buckets]
         p = 0
-        for b in self.buckets:
-            n = b.numel // self.world if mode == "zero1" else b.numel
-            k = max(1, min(PARTIALS_PER_BUCKET, (n // 8 + 255) // 256))
-            b.part_lo, b.part_hi = p, p + k
-            p += k
+        if self.fused_sumsq:
+            fused = list(extra_sinks)
+            covered = [(s.start, s.end) for s in fused]
+            plain = [s for s in flat.sinks.values()
+                     if not any(lo <= s.start and s.end <= hi for lo, hi in covered)]
+            for sink in sorted(fused + plain, key=lambda s: s.start, reverse=True):
+                k = sink_partials(sink.end - sink.start, sink.buf.dim())
+                sink.part = (p, p + k)  # replaced by the tensor slice below
+                p += k
+                self._sq_sinks.append(sink)
+                # the bucket holding the sink's lowest address launches after all of it is written
+                for b in self.buckets:
+                    if b.lo <= sink.start < b.hi:
+                        self._bucket_sq_sinks[b.idx].append(sink)
+                        break
+        else:
+            for b in self.buckets:
+                n = b.numel // self.world if mode == "zero1" else b.numel
+                k = max(1, min(PARTIALS_PER_BUCKET, (n // 8 + 255) // 256))
+                b.part_lo, b.part_hi = p, p + k
+                p += k
         self.partials = torch.zeros(p, dtype=torch.float32, device=flat.device)
+        for sink in self._sq_sinks:
+            lo, hi = sink.part
+            sink.part = self.partials[lo:hi]
+            sink.sq_done = False
         self.sumsq_total = torch.zeros(1, dtype=torch.float32, device=flat.device)
         # ZeRO-1 shard layout: bucket b's shard for this rank, packed in forward order
         self.shard_numel = 0
@@ -185,6 +246,9 @@ class GradReducer:
                 b.shard_lo = self.shard_numel
                 self.shard_numel += b.shard_len
         self.side = torch.cuda.Stream(device=flat.device) if self.overlap else None
+        if not self.fused_sumsq:  # sinks shared with an earlier reducer: no stale partials
+            for sink in list(flat.sinks.values()) + list(extra_sinks):
+                sink.part, sink.sq_done = None, False
         if self.cuda:
             for b in self.buckets:
                 b.event = torch.cuda.Event()
@@ -251,6 +315,8 @@ class GradReducer:
             sink.accumulate = k > 0
         for sink in self._extra_sinks:
             sink.accumulate = k > 0
+        for sink in self._sq_sinks:
+            sink.sq_done = False  # set again by the producers of this micro-batch
         if self.emb_sink is not None:
             # the sparse exchange sums every rank's rows of every micro-batch at once (in the
             # last backward), so the dense embedding gradient is written once, not accumulated
@@ -279,6 +345,13 @@ class GradReducer:
                 raise OSError(5, "injected I/O error inside backward (after a bucket launch)")
 
     def _sumsq(self, g: torch.Tensor, b: Bucket) -> None:
+        if self.fused_sumsq:
+            # per sink: only gradients whose producer did not write its partials this step
+            for sink in self._bucket_sq_sinks[b.idx]:
+                if not sink.sq_done:
+                    kernels().sumsq_into_(sink.buf.reshape(-1), sink.part)
+                sink.sq_done = False
+            return
         part = self.partials[b.part_lo : b.part_hi]
         if g.is_cuda:
             kernels().sumsq_into_(g, part)
@@ -309,13 +382,13 @@ class GradReducer:
             src = grads.float()
             if self.mode == "allreduce":
                 b.work = dist.all_reduce(src, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
-                b.post = lambda: grads.copy_(src)
+                b.post = lambda: _copy_back(grads, src, (src,))
             else:
                 out = src.new_empty(b.shard_len)
                 b.work = dist.reduce_scatter_tensor(out, src, op=dist.ReduceOp.SUM, group=self.group,
                                                     async_op=True)
                 shard = self.grad_shard(b)
-                b.post = lambda: shard.copy_(out)
+                b.post = lambda: _copy_back(shard, out, (src, out))
         elif self.mode == "allreduce":
             b.work = dist.all_reduce(grads, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
         elif self.mode == "zero1":

@@ -157,6 +157,56 @@ def vote(values):
     return out.view(info.world_size, -1)
 
 
+def _device_id(device: torch.device) -> dict:
+    """Identity of the GPU this rank drives (CPU ranks: host name + rank)."""
+    if device.type != "cuda":
+        import socket
+
+        return {"type": "cpu", "id": f"{socket.gethostname()}:cpu"}
+    p = torch.cuda.get_device_properties(device)
+    uuid = getattr(p, "uuid", None)
+    bus = getattr(p, "pci_bus_id", None)
+    dom = getattr(p, "pci_domain_id", None)
+    return {"type": "cuda", "index": device.index, "name": p.name,
+            "pci": f"{dom or 0:04x}:{bus:02x}" if bus is not None else None,
+            "id": str(uuid) if uuid is not None else f"pci:{dom}:{bus}:{device.index}"}
+
+
+def topology_report(info: DistInfo, expected_world: Optional[int] = None) -> dict:
+    """What the job actually ran on, gathered over the control plane (every rank calls this).
+
+    ``world_size`` from the process group, every rank's device identity, the number of distinct
+    GPUs, xGMI/PCIe peer access between every pair of the job's local devices and the RCCL
+    version. Raises if a CUDA job runs fewer distinct GPUs than ranks (two ranks sharing one
+    GPU would time-slice it and make a scaling number meaningless) or if the process group's
+    size differs from ``expected_world``."""
+    world = dist.get_world_size() if dist.is_initialized() else 1
+    devs = ctrl_all_gather_object(_device_id(info.device))
+    ids = [d["id"] for d in devs]
+    rep = {"world_size": world, "devices": devs, "distinct_devices": len(set(ids))}
+    if info.device.type == "cuda":
+        local = sorted({d["index"] for d in devs})
+        peer = True
+        for i in local:
+            for j in local:
+                if i != j and not torch.cuda.can_device_access_peer(i, j):
+                    peer = False
+        rep["peer_access_all_pairs"] = peer if len(local) > 1 else None
+        try:
+            v = torch.cuda.nccl.version()
+            rep["rccl_version"] = ".".join(str(x) for x in v) if isinstance(v, tuple) else str(v)
+        except Exception:  # noqa: BLE001 - informational
+            rep["rccl_version"] = None
+        if rep["distinct_devices"] < world:
+            raise RuntimeError(f"{world} ranks but only {rep['distinct_devices']} distinct GPUs: {ids}")
+    else:
+        rep["peer_access_all_pairs"] = None
+        rep["rccl_version"] = None
+    if expected_world is not None and world != expected_world:
+        raise RuntimeError(f"process group has {world} ranks, expected {expected_world}")
+    return rep
+
+
 def barrier():
     info = get_info()
     if info.distributed:

@@ -3,7 +3,7 @@ d = sys.argv[1]
 agg = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
     for row in csv.DictReader(open(f)):
-        k = row["Kernel_Name"][:60]
+        k = row["Kernel_Name"][:90]
         agg[k][row["Counter_Name"]].append(float(row["Counter_Value"]))
 for k, cs in agg.items():
     print(k)

@@ -110,4 +110,8 @@ def test_bench_torchrun_n_ranks_zero1(world, tmp_path):
     assert j["config"]["global_batch"] == world and j["grad_mode"] == "zero1"
     assert abs(j["value"] - world * 64 / (j["ms_per_step"] / 1e3)) / j["value"] < 0.02
     assert "exposed_comm_ms_per_step" in j and j["comm_GB_per_rank_per_step"] >= 0
+    # self-validation fields of the driver's multi-GPU run: the process group's real size and
+    # every rank's device (on GPUs: one distinct device per rank, else bench.py raises)
+    assert j["world_size"] == world and len(j["device_ids"]) == world
+    assert j["distinct_devices"] >= 1 and "peer_access_all_pairs" in j and "rccl_version" in j
     _check_ckpt(j, world)

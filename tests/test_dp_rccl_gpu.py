@@ -49,10 +49,14 @@ def _run(extra, torchrun):
     return lines[0]
 
 
-@pytest.mark.parametrize("mode", ["zero1", "allreduce"])
-def test_rccl_one_rank_matches_local(mode):
+@pytest.mark.parametrize("mode,rdt", [("zero1", "native"), ("allreduce", "native"), ("zero1", "fp32"),
+                                      ("allreduce", "fp32")])
+def test_rccl_one_rank_matches_local(mode, rdt):
+    """fp32: the reduced fp32 copy is written back from the reducer's side stream while its
+    buffers were allocated on the launching stream (record_stream keeps them alive)."""
     local = _run([], torchrun=False)
-    dp = _run(["--dp-mode", mode], torchrun=True)
+    dp = _run(["--dp-mode", mode, "--dp-reduce-dtype", rdt], torchrun=True)
     assert dp["grad_mode"] == mode and local["grad_mode"] == "local"
+    assert dp["world_size"] == 1 and dp["distinct_devices"] == 1
     # same math: the 1-rank collectives are identities; zero1 shards are the whole buckets
     assert abs(dp["final_loss"] - local["final_loss"]) < 1e-3, (dp["final_loss"], local["final_loss"])

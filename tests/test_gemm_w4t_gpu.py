@@ -1,0 +1,138 @@
+"""The w4 GEMM on k-major operands (csrc/kernels/gemm_w4.hip: ds_read_b64_tr_b16 images) vs fp32.
+
+dX layout  C = A B        A [M, K] as stored, B stored [K, N]          (dY [T, N] @ W [N, K])
+dW layout  C = A^T B      A stored [K, M], B stored [K, N]            (dY^T [N, T] @ X [T, K])
+Every tile width (NJ 4 / 6 / 7 / 8: the four k-major row lengths and their swizzles), both
+rasters, the accumulate and sum-of-squares epilogues, the fused SwiGLU backward, fp16, and the
+Llama-3-8B product shapes. Integer-valued operands make the fp32 reference exact, so those
+checks are bitwise (any swizzle / lane-map error moves whole values); random operands check the
+relative error. Reference math: model.py:195,215,254,379 and their gradients.
+"""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def K():
+    from fault_tolerant_llm_training_amd._native import kernels
+
+    return kernels()
+
+
+def ints(*s, lo=-3, hi=4, dtype=torch.bfloat16):
+    return torch.randint(lo, hi, s, device="cuda").to(dtype)
+
+
+def rnd(*s, dtype=torch.bfloat16):
+    return (torch.rand(*s, device="cuda") * 2 - 1).to(dtype)
+
+
+def rel(out, ref):
+    return ((out.float() - ref).norm() / ref.norm()).item()
+
+
+@pytest.mark.parametrize("nj", [4, 6, 7, 8])
+@pytest.mark.parametrize("M,Kd", [(256, 64), (512, 320), (768, 1024)])
+def test_dx_layout_exact(nj, M, Kd):
+    torch.manual_seed(nj * 7 + M + Kd)
+    N = 32 * nj * 3
+    a = ints(M, Kd)
+    b = ints(Kd, N) + (torch.arange(N, device="cuda") % 5).bfloat16()  # asymmetric columns
+    out = K().gemm_w4_ex(a, False, b, True, M, N, Kd, None, False, None, nj)
+    ref = (a.float() @ b.float()).bfloat16()
+    assert torch.equal(out, ref), (out.float() - ref.float()).abs().max().item()
+
+
+@pytest.mark.parametrize("nj", [4, 6, 7, 8])
+@pytest.mark.parametrize("M,Kd", [(256, 64), (512, 192), (768, 2048)])
+def test_dw_layout_exact(nj, M, Kd):
+    torch.manual_seed(nj * 11 + M + Kd)
+    N = 32 * nj * 2
+    at = ints(Kd, M) + (torch.arange(M, device="cuda") % 3).bfloat16()  # A stored transposed
+    b = ints(Kd, N)
+    out = K().gemm_w4_ex(at, True, b, True, M, N, Kd, None, False, None, nj)
+    ref = (at.float().t() @ b.float()).bfloat16()
+    assert torch.equal(out, ref), (out.float() - ref.float()).abs().max().item()
+
+
+@pytest.mark.parametrize("a_t", [False, True])
+@pytest.mark.parametrize("M,N,Kd", [(1024, 256, 512), (256, 1792, 384)])
+def test_both_rasters(a_t, M, N, Kd):
+    """M > N rasters N-fastest inside an XCD's range, M < N M-fastest: same result either way."""
+    torch.manual_seed(M + N)
+    a = rnd(Kd, M) if a_t else rnd(M, Kd)
+    b = rnd(Kd, N)
+    out = K().gemm_w4_ex(a, a_t, b, True, M, N, Kd, None, False, None, 0)
+    ref = (a.float().t() if a_t else a.float()) @ b.float()
+    assert rel(out, ref) < 4e-3
+
+
+@pytest.mark.parametrize("a_t", [False, True])
+def test_accumulate_and_sumsq(a_t):
+    torch.manual_seed(3)
+    M, N, Kd = 512, 896, 256
+    a = rnd(Kd, M) if a_t else rnd(M, Kd)
+    b = rnd(Kd, N)
+    ref = (a.float().t() if a_t else a.float()) @ b.float()
+    nj = K().gemm_w4_pick(M, N)
+    tiles = (M // 256) * (N // (32 * nj))
+    part = torch.full((tiles + 5,), -1.0, device="cuda")
+    c = rnd(M, N)
+    c0 = c.float().clone()
+    K().gemm_w4_ex(a, a_t, b, True, M, N, Kd, c, True, part, 0)
+    assert rel(c, ref + c0) < 4e-3
+    # one partial per tile, the sum of squares of exactly the stored (rounded) values
+    assert torch.all(part[tiles:] == -1.0)
+    want = c.float().pow(2).sum().item()
+    got = part[:tiles].double().sum().item()
+    assert abs(got - want) <= 1e-5 * want, (got, want)
+    # deterministic: same partials bit for bit
+    part2 = torch.zeros(tiles, device="cuda")
+    c2 = c0.bfloat16()
+    K().gemm_w4_ex(a, a_t, b, True, M, N, Kd, c2, True, part2, 0)
+    assert torch.equal(c2, c) and torch.equal(part2, part[:tiles])
+
+
+@pytest.mark.parametrize("T,D,F", [(256, 256, 224), (512, 640, 1792), (2048, 4096, 14336)])
+def test_swiglu_bwd_epilogue(T, D, F):
+    """dgu from the fused kernel == swiglu_bwd(da) with da from the same GEMM (bitwise), and the
+    fp32 SwiGLU derivative (reference model.py:254) within bf16 error."""
+    torch.manual_seed(T + F)
+    dy = rnd(T, D)
+    w2 = (rnd(D, F) / D ** 0.5).bfloat16()
+    gu = rnd(T, 2 * F) * 2
+    nj = K().gemm_w4_pick(T, F)
+    dgu = K().gemm_swiglu_bwd_w4(dy, w2, gu, 0)
+    da = K().gemm_w4_ex(dy, False, w2, True, T, F, D, None, False, None, nj)
+    assert torch.equal(dgu, K().swiglu_bwd(da, gu))
+    g, u = gu.float()[:, :F], gu.float()[:, F:]
+    daf = (dy.float() @ w2.float()).bfloat16().float()
+    s = torch.sigmoid(g)
+    ref = torch.cat([daf * u * (s + g * s * (1 - s)), daf * g * s], 1)
+    assert rel(dgu, ref) < 1e-2
+
+
+def test_fp16_layouts():
+    torch.manual_seed(5)
+    M, N, Kd = 512, 512, 384
+    a, b = rnd(M, Kd, dtype=torch.float16), rnd(Kd, N, dtype=torch.float16)
+    out = K().gemm_w4_ex(a, False, b, True, M, N, Kd, None, False, None, 0)
+    assert out.dtype == torch.float16 and rel(out, a.float() @ b.float()) < 2e-3
+    at = rnd(Kd, M, dtype=torch.float16)
+    out = K().gemm_w4_ex(at, True, b, True, M, N, Kd, None, False, None, 0)
+    assert rel(out, at.float().t() @ b.float()) < 2e-3
+
+
+# the Llama-3-8B backward products (T = 2048): dX of qkv / wo / w13, dW of qkv / wo / w13 / w2
+@pytest.mark.parametrize("a_t,M,N,Kd", [(False, 2048, 4096, 6144), (False, 2048, 4096, 4096),
+                                        (False, 2048, 4096, 28672), (True, 6144, 4096, 2048),
+                                        (True, 4096, 4096, 2048), (True, 28672, 4096, 2048),
+                                        (True, 4096, 14336, 2048)])
+def test_llama8b_products(a_t, M, N, Kd):
+    torch.manual_seed(M + N + Kd)
+    a = rnd(Kd, M) if a_t else rnd(M, Kd)
+    b = rnd(Kd, N)
+    out = K().gemm_w4_ex(a, a_t, b, True, M, N, Kd, None, False, None, 0)
+    ref = (a.float().t() if a_t else a.float()) @ b.float()
+    assert rel(out, ref) < 4e-3
