@@ -227,7 +227,16 @@ struct Sched {
   static constexpr int dma_slot(int d) { return SB1 + 2 + d * (SB2 - SB1 - 4) / D; }
   static constexpr int OPB = NJ * 4 * PIECE;  // B image
   static constexpr int ST = OPA + OPB;        // stage
+  // LDS: A stage 0 | A stage 1 | B stage 0 | B stage 1, so a stage's offset (32 KiB for A, 4 NJ
+  // KiB for B) plus every fragment / k-step / half offset fits the 16-bit DS immediate: with the
+  // K-tile loop unrolled by two, no fragment read needs an address add
+  static constexpr int A_AT(int st) { return st * OPA; }
+  static constexpr int B_AT(int st) { return 2 * OPA + st * OPB; }
+  static constexpr int B_RD(int st) { return st * OPB; }  // B read bases already hold 2 * OPA
   static_assert(SB2 - SB1 - 4 >= D && SB2 + RS < 2 * MH, "schedule does not fit");
+  // largest DS immediates: stage 1 + k-step 1 + hi half / last fragment (16-bit offset field)
+  static_assert(OPA + 32 * RBA + 4 * RBA < 65536 && OPA + FS * 7 < 65536, "A read offset");
+  static_assert(OPB + 32 * RB + 4 * RB < 65536 && OPB + FS * (NJ - 1) < 65536, "B read offset");
 };
 
 struct Ctx {
@@ -236,14 +245,15 @@ struct Ctx {
   unsigned rdA0, rdA1, rdB0, rdB1;  // K-contiguous images: k-step 0 / 1 lane address
   unsigned aT[8], bT[8];            // k-major images: lane address of fragment i (k-step 0, lo)
   unsigned lds0;
+  unsigned sbase;                   // LDS-DMA: this wave's first piece (m0 base, SGPR)
   unsigned stepA, stepB;            // bytes one K-tile advances the A / B source
   int wid;
 };
 
 // read instruction r (b[0], a[0..7], b[1..NJ-1]; a k-major fragment is two: lo, hi) of k-step KK
-// from the stage at byte offset `stage`
-template <int NJ, bool AT, bool BT, int KK, int r>
-__device__ __forceinline__ void rd(Frag<AT> (&ax)[8], Frag<BT> (&bx)[NJ], const Ctx& c, unsigned stage) {
+// from stage ST (lane base address + immediate)
+template <int NJ, bool AT, bool BT, int KK, int ST, int r>
+__device__ __forceinline__ void rd(Frag<AT> (&ax)[8], Frag<BT> (&bx)[NJ], const Ctx& c) {
   using S = Sched<NJ, AT, BT>;
   constexpr int NA = S::NA, NB = S::NB;
   constexpr bool isA = r >= NB && r < NB + 8 * NA;
@@ -251,11 +261,11 @@ __device__ __forceinline__ void rd(Frag<AT> (&ax)[8], Frag<BT> (&bx)[NJ], const 
     constexpr int i = (r - NB) / NA, h = (r - NB) % NA;
     if constexpr (AT) {
       if constexpr (h == 0)
-        dstr<KK * 32 * RBA>(ax[i].lo, c.aT[i] + stage);
+        dstr<S::A_AT(ST) + KK * 32 * RBA>(ax[i].lo, c.aT[i]);
       else
-        dstr<KK * 32 * RBA + 4 * RBA>(ax[i].hi, c.aT[i] + stage);
+        dstr<S::A_AT(ST) + KK * 32 * RBA + 4 * RBA>(ax[i].hi, c.aT[i]);
     } else {
-      ds16<FS * i>(ax[i].v, (KK ? c.rdA1 : c.rdA0) + stage);
+      ds16<S::A_AT(ST) + FS * i>(ax[i].v, KK ? c.rdA1 : c.rdA0);
     }
   } else {
     constexpr int j = r < NB ? 0 : 1 + (r - NB - 8 * NA) / NB;
@@ -263,33 +273,32 @@ __device__ __forceinline__ void rd(Frag<AT> (&ax)[8], Frag<BT> (&bx)[NJ], const 
     if constexpr (BT) {
       constexpr int RB = S::RB;
       if constexpr (h == 0)
-        dstr<KK * 32 * RB>(bx[j].lo, c.bT[j] + stage);
+        dstr<S::B_RD(ST) + KK * 32 * RB>(bx[j].lo, c.bT[j]);
       else
-        dstr<KK * 32 * RB + 4 * RB>(bx[j].hi, c.bT[j] + stage);
+        dstr<S::B_RD(ST) + KK * 32 * RB + 4 * RB>(bx[j].hi, c.bT[j]);
     } else {
-      ds16<FS * j>(bx[j].v, (KK ? c.rdB1 : c.rdB0) + stage);
+      ds16<S::B_RD(ST) + FS * j>(bx[j].v, KK ? c.rdB1 : c.rdB0);
     }
   }
 }
 
 // the reads of MFMA slot `slot` (RPS instructions) of k-step KK
-template <int NJ, bool AT, bool BT, int KK, int slot>
-__device__ __forceinline__ void rd_slot(Frag<AT> (&ax)[8], Frag<BT> (&bx)[NJ], const Ctx& c, unsigned stage) {
+template <int NJ, bool AT, bool BT, int KK, int ST, int slot>
+__device__ __forceinline__ void rd_slot(Frag<AT> (&ax)[8], Frag<BT> (&bx)[NJ], const Ctx& c) {
   using S = Sched<NJ, AT, BT>;
   sfor<S::RPS>([&](auto QQ) {
     constexpr int r = slot * S::RPS + QQ;
-    if constexpr (r < S::R) rd<NJ, AT, BT, KK, r>(ax, bx, c, stage);
+    if constexpr (r < S::R) rd<NJ, AT, BT, KK, ST, r>(ax, bx, c);
   });
 }
 
-// One K-tile t (stage cur = t & 1): DMA: stage tile t + 2 into this stage; NEXT: read tile t + 1's
-// first k-step.
-template <class E, int NJ, bool AT, bool BT, bool DMA, bool NEXT>
+// One K-tile t in stage CUR = t & 1: DMA: stage tile t + 2 into this stage; NEXT: read tile t + 1's
+// first k-step (stage 1 - CUR).
+template <class E, int NJ, bool AT, bool BT, int CUR, bool DMA, bool NEXT>
 __device__ __forceinline__ void ktile(f32x4_t (&acc)[8][NJ], Frags<NJ, AT, BT>& f, int t, const Ctx& c) {
   using S = Sched<NJ, AT, BT>;
-  const unsigned cur = (unsigned)(t & 1) * S::ST, nxt = (unsigned)((t + 1) & 1) * S::ST;
   const unsigned kofsA = (unsigned)(t + 2) * c.stepA, kofsB = (unsigned)(t + 2) * c.stepB;
-  const unsigned sb = __builtin_amdgcn_readfirstlane(c.lds0 + cur + c.wid * PIECE);
+  const unsigned sb = c.sbase;
   sfor<2 * S::MH>([&](auto SS) {
     constexpr int s = SS;
     constexpr int i = s & 7, j = (s % S::MH) >> 3;  // runs of 8 MFMAs share the B fragment (SrcA)
@@ -307,7 +316,7 @@ __device__ __forceinline__ void ktile(f32x4_t (&acc)[8][NJ], Frags<NJ, AT, BT>& 
       mfma<E>(acc[i][j], val(f.b0[j]), val(f.a0[i]));
     else
       mfma<E>(acc[i][j], val(f.b1[j]), val(f.a1[i]));
-    if constexpr (s < S::RS) rd_slot<NJ, AT, BT, 1, s>(f.a1, f.b1, c, cur);
+    if constexpr (s < S::RS) rd_slot<NJ, AT, BT, 1, CUR, s>(f.a1, f.b1, c);
     if constexpr (s == S::SB1) {  // this stage fully read by every wave -> it may be restaged
       lgkm<0>();
       sfor<8>([&](auto I) { tie(f.a1[I]); });
@@ -322,9 +331,9 @@ __device__ __forceinline__ void ktile(f32x4_t (&acc)[8][NJ], Frags<NJ, AT, BT>& 
           constexpr int qa = d < 2 * NJ ? d / 2 : NJ + (d - 2 * NJ);
           constexpr bool isA = d < 2 * NJ ? (d % 2 == 0) : true;
           if constexpr (isA)
-            dma16<qa * 4 * PIECE>(c.srdA, c.voA[qa], kofsA, sb);
+            dma16<S::A_AT(CUR) + qa * 4 * PIECE>(c.srdA, c.voA[qa], kofsA, sb);
           else
-            dma16<OPA + (d / 2) * 4 * PIECE>(c.srdB, c.voB[d / 2], kofsB, sb);
+            dma16<S::B_AT(CUR) + (d / 2) * 4 * PIECE>(c.srdB, c.voB[d / 2], kofsB, sb);
         }
       });
     }
@@ -336,7 +345,7 @@ __device__ __forceinline__ void ktile(f32x4_t (&acc)[8][NJ], Frags<NJ, AT, BT>& 
         vmcnt<0>();
       barrier();
     }
-    if constexpr (NEXT && s > S::SB2 && s <= S::SB2 + S::RS) rd_slot<NJ, AT, BT, 0, s - S::SB2 - 1>(f.a0, f.b0, c, nxt);
+    if constexpr (NEXT && s > S::SB2 && s <= S::SB2 + S::RS) rd_slot<NJ, AT, BT, 0, 1 - CUR, s - S::SB2 - 1>(f.a0, f.b0, c);
     if constexpr (s == 2 * S::MH - 1) asm volatile("s_setprio 0" ::: "memory");
   });
 }
@@ -406,8 +415,8 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(W4Args p) {
   const unsigned lpart1 = lrowb + (unsigned)(((4 + (lane >> 4)) ^ (lane & 7)) << 4);
   c.rdA0 = c.lds0 + wm * 16 * PIECE + lpart0;
   c.rdA1 = c.lds0 + wm * 16 * PIECE + lpart1;
-  c.rdB0 = c.lds0 + OPA + wn * NJ * 2 * PIECE + lpart0;
-  c.rdB1 = c.lds0 + OPA + wn * NJ * 2 * PIECE + lpart1;
+  c.rdB0 = c.lds0 + 2 * OPA + wn * NJ * 2 * PIECE + lpart0;  // + S::B_RD(stage) as immediate
+  c.rdB1 = c.lds0 + 2 * OPA + wn * NJ * 2 * PIECE + lpart1;
   // fragment reads, k-major: lane 4q + p of 16-lane group g supplies k-row 8 g + q (k-step 0,
   // lo half), columns 4p .. 4p + 3 of the fragment's 16 (byte 8 p of its 32-B pair)
   {
@@ -423,7 +432,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(W4Args p) {
       const int sg = tsw<S::RB>(k0);
 #pragma unroll
       for (int j = 0; j < NJ; ++j)
-        c.bT[j] = c.lds0 + (unsigned)(OPA + k0 * S::RB + 32 * ((wn * NJ + j) ^ sg) + 8 * pp);
+        c.bT[j] = c.lds0 + (unsigned)(2 * OPA + k0 * S::RB + 32 * ((wn * NJ + j) ^ sg) + 8 * pp);
     }
   }
 
@@ -435,31 +444,31 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(W4Args p) {
   Frags<NJ, AT, BT> f;
 
   // prologue: tiles 0 and 1 in flight, then tile 0's k-step-0 fragments
-  const unsigned sb0 = __builtin_amdgcn_readfirstlane(c.lds0 + wid * PIECE);
-  const unsigned sb1 = __builtin_amdgcn_readfirstlane(c.lds0 + S::ST + wid * PIECE);
-  sfor<8>([&](auto Q) { dma16<Q * 4 * PIECE>(c.srdA, c.voA[Q], 0u, sb0); });
-  sfor<NJ>([&](auto Q) { dma16<OPA + Q * 4 * PIECE>(c.srdB, c.voB[Q], 0u, sb0); });
-  if (nk > 1) {
-    sfor<8>([&](auto Q) { dma16<Q * 4 * PIECE>(c.srdA, c.voA[Q], c.stepA, sb1); });
-    sfor<NJ>([&](auto Q) { dma16<OPA + Q * 4 * PIECE>(c.srdB, c.voB[Q], c.stepB, sb1); });
-    vmcnt<S::D>();
-  } else {
-    vmcnt<0>();
-  }
+  c.sbase = __builtin_amdgcn_readfirstlane(c.lds0 + wid * PIECE);
+  const unsigned sb = c.sbase;
+  sfor<8>([&](auto Q) { dma16<S::A_AT(0) + Q * 4 * PIECE>(c.srdA, c.voA[Q], 0u, sb); });
+  sfor<NJ>([&](auto Q) { dma16<S::B_AT(0) + Q * 4 * PIECE>(c.srdB, c.voB[Q], 0u, sb); });
+  sfor<8>([&](auto Q) { dma16<S::A_AT(1) + Q * 4 * PIECE>(c.srdA, c.voA[Q], c.stepA, sb); });
+  sfor<NJ>([&](auto Q) { dma16<S::B_AT(1) + Q * 4 * PIECE>(c.srdB, c.voB[Q], c.stepB, sb); });
+  vmcnt<S::D>();
   barrier();
-  sfor<S::R>([&](auto RR) { rd<NJ, AT, BT, 0, RR>(f.a0, f.b0, c, 0u); });
+  sfor<S::R>([&](auto RR) { rd<NJ, AT, BT, 0, 0, RR>(f.a0, f.b0, c); });
 
   // the zeroed accumulators are MFMA sources next (VALU write -> MFMA SrcC wait states)
   __builtin_amdgcn_sched_barrier(0);
   asm volatile("s_nop 4" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
+  // nk is even (K % 128, checked on the host): K-tiles 0 .. nk - 3 stage tile t + 2, unrolled by
+  // two so every stage offset is static; the last two read what is already staged. (No runtime
+  // branch between alternative tails: with the accumulators live across one the register
+  // allocator spilled them.)
   int t = 0;
-  for (; t + 2 < nk; ++t) ktile<E, NJ, AT, BT, true, true>(acc, f, t, c);
-  if (nk >= 2) {
-    ktile<E, NJ, AT, BT, false, true>(acc, f, t, c);
-    ++t;
+  for (; t + 2 < nk; t += 2) {
+    ktile<E, NJ, AT, BT, 0, true, true>(acc, f, t, c);
+    ktile<E, NJ, AT, BT, 1, true, true>(acc, f, t + 1, c);
   }
-  ktile<E, NJ, AT, BT, false, false>(acc, f, t, c);
+  ktile<E, NJ, AT, BT, 0, false, true>(acc, f, t, c);
+  ktile<E, NJ, AT, BT, 1, false, false>(acc, f, t + 1, c);
   // The accumulators are read by VALU next: wait out the last MFMAs (the compiler does not see
   // the asm as MFMAs, so it inserts no wait states), and keep every accumulator read behind the
   // pad (sched_barrier: register-only instructions may otherwise be hoisted above an asm).
@@ -687,7 +696,7 @@ int pick_nj(long M, long N) {
 
 }  // namespace
 
-// C = A @ B^T (+ residual): A [M, K], B [N, K] bf16 row-major; M % 256, K % 64,
+// C = A @ B^T (+ residual): A [M, K], B [N, K] bf16 row-major; M % 256, K % 128,
 // N % (32 * nj) for a tile width in {256, 224, 192, 128}. nj = 0 picks the width per shape.
 at::Tensor gemm_nt_w4(const at::Tensor& a, const at::Tensor& b, const std::optional<at::Tensor>& out,
                       const std::optional<at::Tensor>& residual, int64_t nj) {
@@ -700,8 +709,8 @@ at::Tensor gemm_nt_w4(const at::Tensor& a, const at::Tensor& b, const std::optio
   const long M = a.size(0), K = a.size(1), N = b.size(0);
   const int NJ = nj > 0 ? (int)nj : pick_nj(M, N);
   TORCH_CHECK(NJ == 8 || NJ == 7 || NJ == 6 || NJ == 4, "gemm_nt_w4: tile width 32 * {8, 7, 6, 4}");
-  TORCH_CHECK(M % BM == 0 && N % (32 * NJ) == 0 && K % BK == 0 && K >= BK, "gemm_nt_w4: M % 256, N % ",
-              32 * NJ, ", K % 64 (got ", M, " ", N, " ", K, ")");
+  TORCH_CHECK(M % BM == 0 && N % (32 * NJ) == 0 && K % (2 * BK) == 0 && K > 0, "gemm_nt_w4: M % 256, N % ",
+              32 * NJ, ", K % 128 (got ", M, " ", N, " ", K, ")");
   TORCH_CHECK(M * K * 2 < (1L << 32) && N * K * 2 < (1L << 32), "gemm_nt_w4: operand over 4 GiB");
   const at::DeviceGuard guard(a.device());
   at::Tensor c;
@@ -757,8 +766,8 @@ at::Tensor gemm_w4_ex(const at::Tensor& a, bool a_t, const at::Tensor& b, bool b
   TORCH_CHECK(a.numel() == M * K && b.numel() == N * K, "gemm_w4_ex: operand sizes do not match M, N, K");
   const int NJ = nj > 0 ? (int)nj : pick_nj(M, N);
   TORCH_CHECK(NJ == 8 || NJ == 7 || NJ == 6 || NJ == 4, "gemm_w4_ex: no tile width fits N = ", N);
-  TORCH_CHECK(M % BM == 0 && N % (32 * NJ) == 0 && K % BK == 0 && K >= BK, "gemm_w4_ex: M % 256, N % ",
-              32 * NJ, ", K % 64 (got ", M, " ", N, " ", K, ")");
+  TORCH_CHECK(M % BM == 0 && N % (32 * NJ) == 0 && K % (2 * BK) == 0 && K > 0, "gemm_w4_ex: M % 256, N % ",
+              32 * NJ, ", K % 128 (got ", M, " ", N, " ", K, ")");
   // 32-bit buffer offsets: the whole operand (a K-tile advance is a scalar offset) under 4 GiB
   TORCH_CHECK(M * K * 2 < (1L << 32) && N * K * 2 < (1L << 32), "gemm_w4_ex: operand over 4 GiB");
   const at::DeviceGuard guard(a.device());
@@ -817,7 +826,7 @@ at::Tensor gemm_qkv_rope_w4(const at::Tensor& x, const at::Tensor& w, const at::
   TORCH_CHECK(d % 8 == 0 && M % seq == 0 && cos_t.size(0) >= seq && cos_t.size(1) == d / 2,
               "gemm_qkv_rope_w4: rope tables / head dim");
   const int NJ = pick_nj(M, N);
-  TORCH_CHECK(NJ > 0 && M % BM == 0 && K % BK == 0, "gemm_qkv_rope_w4: M % 256, K % 64, N % 128");
+  TORCH_CHECK(NJ > 0 && M % BM == 0 && K % (2 * BK) == 0, "gemm_qkv_rope_w4: M % 256, K % 128, N % 128");
   const at::DeviceGuard guard(x.device());
   auto c = at::empty({M, N}, x.options());
   W4Args p{};
@@ -856,7 +865,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> gemm_swiglu_w4(const at::Tensor& 
   const long M = x.size(0), K = x.size(1), F2 = w13.size(0), F = F2 / 2;
   constexpr int NJ = 7, NWC = 16 * NJ;
   TORCH_CHECK(w13.size(1) == K && F2 % 2 == 0, "gemm_swiglu_w4: shape mismatch");
-  TORCH_CHECK(M % BM == 0 && F % NWC == 0 && K % BK == 0 && K >= BK, "gemm_swiglu_w4: M % 256, F % 112, K % 64 (got ",
+  TORCH_CHECK(M % BM == 0 && F % NWC == 0 && K % (2 * BK) == 0 && K > 0, "gemm_swiglu_w4: M % 256, F % 112, K % 128 (got ",
               M, " ", F, " ", K, ")");
   TORCH_CHECK(M * K * 2 < (1L << 32) && F2 * K * 2 < (1L << 32), "gemm_swiglu_w4: operand over 4 GiB");
   const at::DeviceGuard guard(x.device());
@@ -899,8 +908,8 @@ at::Tensor gemm_swiglu_bwd_w4(const at::Tensor& dy, const at::Tensor& w2, const 
   TORCH_CHECK(dy.numel() == M * D && gu.numel() == M * 2 * F, "gemm_swiglu_bwd_w4: shape mismatch");
   const int NJ = nj > 0 ? (int)nj : pick_nj(M, F);
   TORCH_CHECK(NJ == 8 || NJ == 7 || NJ == 6 || NJ == 4, "gemm_swiglu_bwd_w4: no tile width fits F = ", F);
-  TORCH_CHECK(M % BM == 0 && F % (32 * NJ) == 0 && D % BK == 0, "gemm_swiglu_bwd_w4: M % 256, F % ", 32 * NJ,
-              ", D % 64 (got ", M, " ", F, " ", D, ")");
+  TORCH_CHECK(M % BM == 0 && F % (32 * NJ) == 0 && D % (2 * BK) == 0 && D > 0, "gemm_swiglu_bwd_w4: M % 256, F % ",
+              32 * NJ, ", D % 128 (got ", M, " ", F, " ", D, ")");
   TORCH_CHECK(M * D * 2 < (1L << 32) && D * F * 2 < (1L << 32), "gemm_swiglu_bwd_w4: operand over 4 GiB");
   const at::DeviceGuard guard(dy.device());
   auto dgu = at::empty({M, 2 * F}, dy.options());

@@ -1,10 +1,15 @@
 """Causal GQA flash attention on packed projections (gfx950 HIP kernels).
 
-Inputs are the rotated ``qk`` buffer ``[T, (Hq+Hkv)*D]`` written by the RoPE
-kernel and the fused ``qkv`` projection ``[T, (Hq+2Hkv)*D]`` (V is read in
-place). KV heads are indexed as ``h // (Hq/Hkv)`` inside the kernel, so the
-reference's materialised ``repeat_kv`` (model.py:129-138) and the
-transpose/contiguous copies (model.py:207-213) never exist.
+Q and K come rotated (reference model.py:100-126) from one of two producers:
+by default the QKV projection's GEMM epilogue (``gemm_qkv_rope_w4``, csrc/kernels/gemm_w4.hip)
+rotates them in place, so ``qk`` IS the packed ``qkv`` projection ``[T, (Hq+2Hkv)*D]``; on the
+paths without that epilogue (fp32, GPT-2-sized models, FT_QKV_ROPE=0) the RoPE kernel
+(csrc/kernels/rope.hip) writes a separate rotated ``qk`` buffer ``[T, (Hq+Hkv)*D]``. V is always
+read in place from ``qkv``. KV heads are indexed as ``h // (Hq/Hkv)`` inside the kernels, so
+the reference's materialised ``repeat_kv`` (model.py:129-138) and the transpose/contiguous
+copies (model.py:207-213) never exist. This module picks the kernel family by dtype
+(bf16/fp16: csrc/kernels/flash_attn.hip, fp32: csrc/kernels/flash_f32.hip) and exposes the
+deterministic / non-deterministic backward switch.
 """
 from __future__ import annotations
 

@@ -117,7 +117,7 @@ def _w4_fits(x2: torch.Tensor, w: torch.Tensor, max_nj: int = 8) -> bool:
     if _GEMM_MODE == "blas" or not (x2.is_cuda and x2.dtype in _W4_DTYPES and w.dtype == x2.dtype):
         return False
     T, K = x2.shape
-    if T % 256 or K % 64:
+    if T % 256 or K % 128:  # the w4 kernel runs K-tiles of 64 in pairs
         return False
     nj = kernels().gemm_w4_pick(T, w.shape[0])
     # at least half the chip in tiles: smaller products (GPT-2-sized, K = 768-1024) are
@@ -189,7 +189,7 @@ def _w4t_fits(M: int, N: int, K: int, *ts) -> bool:
     if not (_W4_BWD and _GEMM_MODE != "blas" and all(t.is_cuda and t.dtype in _W4_DTYPES for t in ts)
             and len({t.dtype for t in ts}) == 1):
         return False
-    if M % 256 or K % 64 or K < 64:
+    if M % 256 or K % 128 or K < 128:  # K-tiles of 64 in pairs
         return False
     nj = kernels().gemm_w4_pick(M, N)
     return 0 < nj and (M // 256) * (N // (32 * nj)) >= _W4_MIN_TILES
@@ -226,7 +226,7 @@ def _use_tn(dy2: torch.Tensor, x2: torch.Tensor) -> bool:
     K = x2.shape[1]
     if T % 64 or N % 64 or K % 64:
         return False
-    if _W4_DW and T % 64 == 0 and N % 256 == 0 and kernels().gemm_w4_pick(N, K) > 0:
+    if _W4_DW and T % 128 == 0 and N % 256 == 0 and kernels().gemm_w4_pick(N, K) > 0:
         return True  # the w4 kernel runs dW on the transposed (K-contiguous) operands
     return _DW_MODE == "all" or 2.0 * T * N * K >= _DW_MIN_FLOP
 
@@ -785,14 +785,14 @@ def set_w4_swiglu(on: bool) -> None:
 
 
 def _swiglu_w4_ok(x2: torch.Tensor, w13: torch.Tensor) -> bool:
-    """Fused path: bf16 on the GPU, w4 tile shapes (T % 256, F % 112, K % 64), at least half the
+    """Fused path: bf16 on the GPU, w4 tile shapes (T % 256, F % 112, K % 128), at least half the
     chip in tiles, and the transposed-operand weight-gradient path (which consumes a^T)."""
     if not (_W4_SWIGLU and _W4_FWD and _GEMM_MODE != "blas" and x2.is_cuda and x2.dtype == torch.bfloat16
             and w13.dtype == x2.dtype and not _FFN_T_ONLY):
         return False
     T, K = x2.shape
     F = w13.shape[0] // 2
-    if T % 256 or K % 64 or F % 112 or (T // 256) * (F // 112) < _W4_MIN_TILES:
+    if T % 256 or K % 128 or F % 112 or (T // 256) * (F // 112) < _W4_MIN_TILES:
         return False
     return _DW_MODE == "all" or (_DW_MODE != "none" and 2.0 * T * 2 * F * K >= _DW_MIN_FLOP)
 
@@ -806,7 +806,7 @@ def _ffn_w4t_ok(x2: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor) -> bool:
         return False
     T, D = x2.shape
     F = w2.shape[1]
-    if T % 256 or D % 64 or F % 112 or (T // 256) * (F // 112) < _W4_MIN_TILES:
+    if T % 256 or D % 128 or F % 112 or (T // 256) * (F // 112) < _W4_MIN_TILES:
         return False
     return (_w4t_fits(T, F, D, x2, w2) and _w4t_fits(2 * F, D, T, x2) and _w4t_fits(D, F, T, x2)
             and _w4t_fits(T, D, 2 * F, x2))

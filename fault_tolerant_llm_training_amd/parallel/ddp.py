@@ -233,10 +233,13 @@ class GradReducer:
                 b.part_lo, b.part_hi = p, p + k
                 p += k
         self.partials = torch.zeros(p, dtype=torch.float32, device=flat.device)
+        self._sq_slices = []
         for sink in self._sq_sinks:
             lo, hi = sink.part
             sink.part = self.partials[lo:hi]
             sink.sq_done = False
+            self._sq_slices.append(sink.part)
+        self._sq_slice_of = {id(s): t for s, t in zip(self._sq_sinks, self._sq_slices)}
         self.sumsq_total = torch.zeros(1, dtype=torch.float32, device=flat.device)
         # ZeRO-1 shard layout: bucket b's shard for this rank, packed in forward order
         self.shard_numel = 0
@@ -344,12 +347,19 @@ class GradReducer:
                 self.fault_after_buckets = 0  # test hook (trainer FT_INJECT_FAULT=r:s:backward)
                 raise OSError(5, "injected I/O error inside backward (after a bucket launch)")
 
+    def set_producer_sums(self, on: bool) -> None:
+        """A/B switch (scripts/ab_step.py): the gradient producers write the norm partials (on) or
+        every sink gets the separate sum-of-squares pass (off). Fused-sumsq reducers only."""
+        for sink, part in zip(self._sq_sinks, self._sq_slices):
+            sink.part = part if on else None
+            sink.sq_done = False
+
     def _sumsq(self, g: torch.Tensor, b: Bucket) -> None:
         if self.fused_sumsq:
             # per sink: only gradients whose producer did not write its partials this step
             for sink in self._bucket_sq_sinks[b.idx]:
                 if not sink.sq_done:
-                    kernels().sumsq_into_(sink.buf.reshape(-1), sink.part)
+                    kernels().sumsq_into_(sink.buf.reshape(-1), self._sq_slice_of[id(sink)])
                 sink.sq_done = False
             return
         part = self.partials[b.part_lo : b.part_hi]

@@ -262,9 +262,21 @@ def train(args) -> int:
         restore_model(model, checkpoint["model"])
         logger.info("Model loaded from checkpoint")
     if args.compile:
-        # the reference's line (train.py:62), qualified: nothing is traced or recompiled here
-        logger.info("Using `torch.compile` — accepted for CLI compatibility, not applied: the step "
-                    "already runs fused gfx950 kernels")
+        # The reference compiles the model (train.py:61-63) to cut launch overhead and fuse ops.
+        # Here the ops are already fused gfx950 kernels; what is left to "compile" is the launch
+        # sequence, and the MI355X-native form of that is the whole-step HIP graph (--hip-graph):
+        # on one GPU without gradient accumulation --compile turns it on. Elsewhere the graph
+        # cannot capture the step (collectives / host-side accumulation), so the flag is accepted
+        # and logged as not applied.
+        if device.type == "cuda" and not info.distributed and max(1, int(args.grad_accum)) == 1:
+            logger.info("Using `torch.compile`")
+            logger.info("`torch.compile` -> whole-step HIP graph capture (--hip-graph): the step's "
+                        "kernel launches are recorded once and replayed")
+            args.hip_graph = True
+        else:
+            logger.info("Using `torch.compile` — accepted for CLI compatibility, not applied: the step "
+                        "already runs fused gfx950 kernels and the whole-step HIP graph needs one GPU "
+                        "without gradient accumulation")
     model.train()
 
     # AdamW moments default to the model dtype like the reference, except under fp16: the second
@@ -631,6 +643,13 @@ def train(args) -> int:
         boundary(final=True)  # drains the loss log, last non-finite check, last signals
         if ckpt["engine"] is not None:
             ckpt["engine"].wait()
+        if getattr(args, "state_digest", False):
+            from .utils.digest import state_digest
+
+            dg = state_digest(model.flat.params, optimizer.exp_avg, optimizer.exp_avg_sq)
+            logger.info(f"[rank {info.rank}] State digest at step {training_step}: params={dg['params']} "
+                        f"exp_avg={dg['exp_avg']} exp_avg_sq={dg['exp_avg_sq']} "
+                        f"optimizer_step={optimizer.step_count} data_loader={json.dumps(loader.state_dict(), sort_keys=True)}")
         logger.info("Training completed")
     except _StopTraining as stop:
         e = stop.cause

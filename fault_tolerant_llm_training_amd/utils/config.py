@@ -116,6 +116,12 @@ def build_parser() -> argparse.ArgumentParser:
     )
     parser.add_argument("--seed", type=int, default=1234, help="RNG seed for init and data")
     parser.add_argument(
+        "--state-digest",
+        action="store_true",
+        help="At 'Training completed', log bit-level digests of the parameters, AdamW moments and "
+        "data-loader position (resume-equivalence checks without a second checkpoint on disk)",
+    )
+    parser.add_argument(
         "--device", type=str, default="cuda", choices=["cuda", "cpu"], help="Run on GPU (default) or CPU"
     )
     parser.add_argument(

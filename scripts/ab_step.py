@@ -19,6 +19,11 @@ Knobs toggled between timing windows (alternating rounds, so box and clock drift
   fastmath — AdamW / SwiGLU with the hardware v_rcp_f32 / v_sqrt_f32 instead of IEEE division/sqrt
   w4wide — the wide forward products (w13 at 224, the LM head at 256 columns) on the w4 GEMM too
   w4swiglu — the w1|w3 GEMM on the w4 kernel with SwiGLU in its epilogue (no separate SwiGLU pass)
+  w4bwd — every dX / dW (and the FFN backward with the SwiGLU-backward epilogue) on the w4 kernel's
+          k-major layouts (round 4) instead of hipBLASLt + transposed copies
+  psums — the gradient-norm partials written by the dW / norm epilogues instead of a sumsq pass
+  w4head — the LM-head logits GEMM on the w4 kernel
+  r4    — w4bwd + psums + w4head together (round-4 routing vs round-3)
 Usage: python scripts/ab_step.py [--steps 8] [--rounds 3] [--configs gemm,dw ...]
 """
 from __future__ import annotations
@@ -121,6 +126,11 @@ def main():
                "notrans": lambda on: setattr(Fx, "_DW_MODE", "none" if on else "auto"),
                "fastmath": lambda on: (torch.cuda.synchronize(), kernels().set_exact_math(not on)),
                "w4swiglu": lambda on: (torch.cuda.synchronize(), Fx.set_w4_swiglu(on)),
+               "w4bwd": lambda on: (torch.cuda.synchronize(), Fx.set_w4_bwd(on)),
+               "psums": lambda on: (torch.cuda.synchronize(), red.set_producer_sums(on)),
+               "w4head": lambda on: (torch.cuda.synchronize(), Fx.set_w4_head(on)),
+               "r4": lambda on: (torch.cuda.synchronize(), Fx.set_w4_bwd(on), red.set_producer_sums(on),
+                                 Fx.set_w4_head(on)),
                "w4wide": lambda on: (torch.cuda.synchronize(), setattr(Fx, "_W4_FWD_MAX_NJ", 8 if on else 6))}
     configs = list(itertools.product([False, True], repeat=len(knobs)))
 

@@ -20,6 +20,10 @@ from collections import defaultdict
 def family(name: str) -> str:
     if name.startswith("Cijk") or name.startswith("Custom_Cijk"):
         return "gemm(hipBLASLt)"
+    m = re.search(r"gemm_w4_kernel<\w+, (\d+), (\d+), (\w+), (\w+)>", name)
+    if m:  # NJ, epilogue, k-major A, k-major B
+        lay = {("false", "false"): "fwd", ("false", "true"): "dX", ("true", "true"): "dW"}.get((m.group(3), m.group(4)), "?")
+        return f"gemm_w4 {lay} nj{m.group(1)} epi{m.group(2)}"
     m = re.search(r"\(anonymous namespace\)::(\w+)", name)
     if m:
         return m.group(1)

@@ -188,3 +188,28 @@ def test_background_preallocation_cpu(tmp_path):
     c = torch.load(path, map_location="cpu", weights_only=True)
     for k, v in m.state_dict().items():
         assert torch.equal(c["model"][k], v), k
+
+
+@pytest.mark.parametrize("src,dst", [(torch.float16, torch.float32), (torch.float32, torch.float16)])
+def test_moment_dtype_converts_on_load(tmp_path, src, dst):
+    """fp16 models keep fp32 AdamW moments by default (the reference keeps them in the model dtype,
+    docs/PARITY.md): a checkpoint written with the other moment dtype — an fp16-moment file from an
+    earlier / reference-style run, or the reverse — loads with the values converted, both through
+    the flat fast path and the per-tensor path."""
+    a = model_args_for("tiny", vocab_size=96, seq_len=16)
+    m = build_model(a, "cpu", torch.float16, seed=4)
+    opt = FlatAdamW(m.parameters(), m.flat, lr=1e-3, max_grad_norm=1.0, state_dtype=src)
+    tok = torch.randint(0, 96, (2, 16))
+    m(tok, tok).backward()
+    opt.step()
+    path = str(tmp_path / "m.ckpt")
+    s = build_lr_scheduler(opt, 3)
+    _engine(m, opt).save(path, lambda host: build_checkpoint(m, opt, s, 1, host), blocking=True)
+    c = load_checkpoint(path)
+    assert c["optimizer"]["state"][0]["exp_avg"].dtype == src
+    m2 = build_model(a, "cpu", torch.float16, seed=5)
+    opt2 = FlatAdamW(m2.parameters(), m2.flat, lr=1e-3, max_grad_norm=1.0, state_dtype=dst)
+    opt2.load_state_dict(c["optimizer"])
+    assert opt2.exp_avg.dtype == dst
+    assert torch.equal(opt2.exp_avg, opt.exp_avg.to(dst)) and torch.equal(opt2.exp_avg_sq, opt.exp_avg_sq.to(dst))
+    assert opt2.step_count == opt.step_count

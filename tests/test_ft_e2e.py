@@ -149,6 +149,34 @@ def test_resume_is_bit_exact(tmp_path, source):
     _assert_same_state(_final_state(_ckpt(d, "10")), _final_state(_ckpt(d, "30")))
 
 
+def _digest(out):
+    m = re.search(r"State digest at step (\d+): (.*)", out)
+    assert m, out[-3000:]
+    return int(m.group(1)), m.group(2).strip()
+
+
+def test_state_digest_resume_equivalence_iterable(tmp_path):
+    """--state-digest (the full-scale form of the check above: no second checkpoint on disk): the
+    uninterrupted and the interrupted-then-resumed iterable-dataset runs log identical digests of
+    parameters, moments, optimizer step and data-loader position; a different run does not."""
+    d = str(tmp_path)
+    write_fake_sbatch(d)
+    pq = os.path.join(d, "data.parquet")
+    make_parquet(pq, n_docs=30)
+    base = (TINY + ["--dataset", pq, "--tokenizer-name-or-path", "byte", "--iterable-dataset", "--state-digest"]
+            + _common(d) + ["--training-steps", "11", "--lr-warmup-steps", "4"])
+    rc, out = run_train(d, "40", base)
+    assert rc == 0 and "Training completed" in out, out[-3000:]
+    ref = _digest(out)
+    rc, out = run_train(d, "41", base + ["--raise-error", "--error-step", "6"])
+    assert rc == 0 and "Checkpoint saved at step 6" in out
+    rc, out = run_train(d, "42", base + ["--checkpoint-id", "41"])
+    assert rc == 0 and "Resuming training from training_step 6" in out, out[-3000:]
+    assert _digest(out) == ref and ref[0] == 11
+    rc, out = run_train(d, "43", base + ["--seed", "99"])
+    assert rc == 0 and _digest(out)[1] != ref[1]
+
+
 def test_sigusr1_preempt_resume_loses_zero_steps(tmp_path):
     """Preempt at an arbitrary moment with SIGUSR1, resume, compare with the uninterrupted run."""
     d = str(tmp_path)

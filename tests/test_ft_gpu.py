@@ -118,3 +118,41 @@ def test_gpu_nonfinite_gradient_saves_state_before_the_bad_step(tmp_path):
     rc, out2 = run_train(d, "731", base + ["--raise-error", "--error-step", str(n)], timeout=240)
     assert rc == 0 and f"Checkpoint saved at step {n}" in out2, out2[-3000:]
     _same(_load(d, 730), _load(d, 731))
+
+
+@pytest.mark.timeout(900)
+def test_gpu_llama8b_iterable_error_resume_bit_exact(tmp_path):
+    """BASELINE config 4 at its scale: Llama-3-8B, seq 2048, the packing IterableParquetDataset
+    (reference dataset.py:56-101, byte tokenizer on a generated parquet; train.py:36-39's
+    fast-forward is the dataset's mid-shard state here). An injected error at step 5 saves the
+    48 GB state; the resumed job runs to step 12 and must end with exactly the parameters, AdamW
+    moments, optimizer step and data-loader position of an uninterrupted run to step 12 (bit-level
+    digests, --state-digest: one checkpoint on disk instead of three)."""
+    import re
+
+    from helpers import make_parquet
+
+    d = str(tmp_path)
+    write_fake_sbatch(d)
+    pq = os.path.join(d, "train.parquet")
+    make_parquet(pq, n_docs=5000, seed=3)
+    base = ["--device", "cuda", "--model", "llama3-8b", "--dataset", pq, "--iterable-dataset",
+            "--tokenizer-name-or-path", "byte", "--vocab-size", "131072", "--sequence-length", "2048",
+            "--batch-size", "1", "--learning-rate", "5e-5", "--lr-warmup-steps", "100", "--logging-frequency", "4",
+            "--checkpoint-path", os.path.join(d, "ck"), "--training-steps", "12", "--state-digest"]
+
+    def digest(out):
+        m = re.search(r"State digest at step (\d+): (.*)", out)
+        assert m, out[-3000:]
+        return int(m.group(1)), m.group(2).strip()
+
+    rc, out = run_train(d, "790", base, timeout=600)
+    assert rc == 0 and "Training completed" in out, out[-3000:]
+    ref = digest(out)
+    assert ref[0] == 12
+    rc, out = run_train(d, "791", base + ["--raise-error", "--error-step", "5"], timeout=600)
+    assert rc == 0 and "Checkpoint saved at step 5" in out, out[-3000:]
+    rc, out = run_train(d, "792", base + ["--checkpoint-id", "791"], timeout=600)
+    assert rc == 0 and "Resuming training from training_step 5" in out, out[-3000:]
+    assert "Data loader position restored" in out
+    assert digest(out) == ref

@@ -33,7 +33,7 @@ def rel(out, ref):
 
 
 @pytest.mark.parametrize("nj", [4, 6, 7, 8])
-@pytest.mark.parametrize("M,Kd", [(256, 64), (512, 320), (768, 1024)])
+@pytest.mark.parametrize("M,Kd", [(256, 128), (512, 384), (768, 1024)])
 def test_dx_layout_exact(nj, M, Kd):
     torch.manual_seed(nj * 7 + M + Kd)
     N = 32 * nj * 3
@@ -45,7 +45,7 @@ def test_dx_layout_exact(nj, M, Kd):
 
 
 @pytest.mark.parametrize("nj", [4, 6, 7, 8])
-@pytest.mark.parametrize("M,Kd", [(256, 64), (512, 192), (768, 2048)])
+@pytest.mark.parametrize("M,Kd", [(256, 128), (512, 256), (768, 2048)])
 def test_dw_layout_exact(nj, M, Kd):
     torch.manual_seed(nj * 11 + M + Kd)
     N = 32 * nj * 2
@@ -94,7 +94,7 @@ def test_accumulate_and_sumsq(a_t):
     assert torch.equal(c2, c) and torch.equal(part2, part[:tiles])
 
 
-@pytest.mark.parametrize("T,D,F", [(256, 256, 224), (512, 640, 1792), (2048, 4096, 14336)])
+@pytest.mark.parametrize("T,D,F", [(256, 256, 224), (512, 768, 1792), (2048, 4096, 14336)])
 def test_swiglu_bwd_epilogue(T, D, F):
     """dgu from the fused kernel == swiglu_bwd(da) with da from the same GEMM (bitwise), and the
     fp32 SwiGLU derivative (reference model.py:254) within bf16 error."""
@@ -111,6 +111,13 @@ def test_swiglu_bwd_epilogue(T, D, F):
     s = torch.sigmoid(g)
     ref = torch.cat([daf * u * (s + g * s * (1 - s)), daf * g * s], 1)
     assert rel(dgu, ref) < 1e-2
+
+
+def test_k_must_pair():
+    """K-tiles run in pairs (static LDS stage offsets): K % 128 is checked, not silently wrong."""
+    a, b = rnd(256, 192), rnd(192, 256)
+    with pytest.raises(RuntimeError, match="K % 128"):
+        K().gemm_w4_ex(a, False, b, True, 256, 256, 192, None, False, None, 0)
 
 
 def test_fp16_layouts():

@@ -102,3 +102,37 @@ def test_train_py_hip_graph_matches_eager_and_saves(tmp_path):
 
     la = re.findall(r"Training step: (\d+) \| Loss: ([0-9.]+)", out)
     assert len(la) >= 15
+
+
+def test_train_py_compile_is_the_hip_graph_and_resumes_bit_exact(tmp_path):
+    """train.py --compile (reference train.py:61-63) on one GPU = the whole-step HIP graph: the
+    reference's log line, graph replays, an injected error saves, the resumed --compile job ends
+    bit-identical (params, both moments, scheduler) to an uninterrupted eager run."""
+    import os
+
+    from helpers import run_train, write_fake_sbatch
+
+    d = str(tmp_path)
+    write_fake_sbatch(d)
+    ck = os.path.join(d, "ck")
+    base = ["--device", "cuda", "--model", "tiny", "--synthetic-data", "--vocab-size", "1024",
+            "--sequence-length", "256", "--batch-size", "2", "--learning-rate", "1e-3", "--lr-warmup-steps", "3",
+            "--logging-frequency", "5", "--checkpoint-path", ck, "--training-steps", "40", "--raise-error"]
+    rc, out = run_train(d, "780", base + ["--error-step", "30"], timeout=240)  # eager reference
+    assert rc == 0 and "Checkpoint saved at step 30" in out, out[-3000:]
+    rc, out = run_train(d, "781", base + ["--compile", "--error-step", "17"], timeout=240)
+    assert rc == 0 and "Using `torch.compile`" in out and "HIP graph" in out, out[-3000:]
+    assert "Checkpoint saved at step 17" in out, out[-3000:]
+    rc, out = run_train(d, "782", base + ["--compile", "--error-step", "30", "--checkpoint-id", "781"], timeout=240)
+    assert rc == 0 and "Resuming training from training_step 17" in out and "HIP graph" in out, out[-3000:]
+    assert "Checkpoint saved at step 30" in out, out[-3000:]
+    load = lambda j: torch.load(os.path.join(ck, f"checkpoint_{j}.ckpt"), map_location="cpu",  # noqa: E731
+                                weights_only=True)
+    a, b = load(780), load(782)
+    assert a["training_step"] == b["training_step"] == 30
+    for k in a["model"]:
+        assert torch.equal(a["model"][k], b["model"][k]), k
+    for i in a["optimizer"]["state"]:
+        for key in ("exp_avg", "exp_avg_sq", "step"):
+            assert torch.equal(a["optimizer"]["state"][i][key], b["optimizer"]["state"][i][key]), (i, key)
+    assert a["lr_scheduler"] == b["lr_scheduler"]
