@@ -1172,11 +1172,14 @@ __global__ __launch_bounds__(64 * NW * SPLIT, SPLIT == 1 ? 4 / NW : 8 / (NW * SP
 // SPLIT = 2 (small grids, see flash_bwd): as the forward's key split, two half-blocks sweep
 // the even / odd key tiles of the same queries and add their dQ partials through LDS (in a
 // fixed order: still bit-reproducible).
+// O != null: the kernel forms delta = rowsum(dO * O) itself (each lane pair already holds its
+// query's dO row) and publishes it for the dK/dV kernel that runs after it — the separate
+// flash_bwd_pre pass and its second read of dO are gone.
 template <class E, int D, int NW = 4, int SPLIT = 1>
 __global__ __launch_bounds__(64 * NW * SPLIT, SPLIT == 1 ? 4 / NW : 8 / (NW * SPLIT)) void flash_bwd_dq_kernel(
     const bf16_t* __restrict__ dO, const bf16_t* __restrict__ qk, const bf16_t* __restrict__ qkv,
-    const float* __restrict__ lse2, const float* __restrict__ delta, bf16_t* __restrict__ dqkv, int B,
-    int S, int Hq, int Hkv, float sl2, float scale, long ldqk_) {
+    const float* __restrict__ lse2, float* __restrict__ delta, bf16_t* __restrict__ dqkv, int B,
+    int S, int Hq, int Hkv, float sl2, float scale, long ldqk_, const bf16_t* __restrict__ O) {
   constexpr int BM = 32 * NW, BN = 64, KS = D / 16, NDB = D / 32;
   constexpr int TILE = BN * D * 2;
   // K | V tiles arrive by LDS-DMA (no staging VGPRs held across the compute: at one wave
@@ -1215,7 +1218,27 @@ __global__ __launch_bounds__(64 * NW * SPLIT, SPLIT == 1 ? 4 / NW : 8 / (NW * SP
     df[ks] = *reinterpret_cast<const typename FA<E>::v8*>(dOg + qr * ldo + ks * 16 + hi * 8);
   }
   const float lq = lse2[((long)b * Hq + h) * stat_stride(S) + qr];
-  const float dlq = delta[((long)b * Hq + h) * stat_stride(S) + qr];
+  float dlq;
+  if (O != nullptr) {  // uniform
+    // delta of this lane's query: its half of the dO . O dot product, plus the other half
+    // from lane ^ 32 (same query, the other 8 of every 16 columns); fp32 like flash_bwd_pre
+    const bf16_t* Og = O + (long)b * S * ldo + (long)h * D + qr * ldo;
+    float acc = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      float x[8], y[8];
+      ld8<E>(Og + ks * 16 + hi * 8, y);
+      const auto dv = df[ks];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x[j] = (float)dv[j];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc += x[j] * y[j];
+    }
+    dlq = acc + __shfl_xor(acc, 32, 64);
+    if (half == 0 && hi == 0 && qrow < S) delta[((long)b * Hq + h) * stat_stride(S) + qrow] = dlq;
+  } else {
+    dlq = delta[((long)b * Hq + h) * stat_stride(S) + qr];
+  }
 
   const int kend = min((qt + 1) * BM, S);
   const int ntiles = (kend + BN - 1) / BN;
@@ -1345,11 +1368,16 @@ __global__ __launch_bounds__(64 * NW * SPLIT, SPLIT == 1 ? 4 / NW : 8 / (NW * SP
   }
 }
 
-// dqkv[:, q | k | v] = bf16(dQ), bf16(sum_G dK_part), bf16(sum_G dV_part)
+// dqkv[:, q | k | v] = bf16(dQ), bf16(sum_G dK_part), bf16(sum_G dV_part).
+// cos_t != null: the Q and K columns are also rotated back (RoPE backward, reference
+// model.py:100-126 transposed: the interleaved pair (x0, x1) times cis(-theta)), so dqkv is the
+// gradient of the unrotated projection and no separate rope_bwd pass runs; dQ written by the
+// deterministic dQ kernel is rotated in place.
 template <class E>
 __global__ __launch_bounds__(256) void flash_bwd_finalize_kernel(
     const float* __restrict__ dq_acc, const bf16_t* __restrict__ dk_part,
-    const bf16_t* __restrict__ dv_part, bf16_t* __restrict__ dqkv, long T, int Hq, int Hkv, int D) {
+    const bf16_t* __restrict__ dv_part, bf16_t* __restrict__ dqkv, long T, int Hq, int Hkv, int D,
+    const float* __restrict__ cos_t, const float* __restrict__ sin_t, int S) {
   const int G = Hq / Hkv;
   const int W = (Hq + 2 * Hkv) * D;
   const int vpr = W / 4;
@@ -1359,8 +1387,13 @@ __global__ __launch_bounds__(256) void flash_bwd_finalize_kernel(
     const int col = (int)(i - t * vpr) * 4;
     float4 v;
     if (col < Hq * D) {
-      if (dq_acc == nullptr) continue;  // dQ already written by the deterministic dQ kernel
-      v = *reinterpret_cast<const float4*>(dq_acc + t * Hq * D + col);
+      if (dq_acc == nullptr) {  // dQ already written by the deterministic dQ kernel
+        if (cos_t == nullptr) continue;
+        const uint2 x = *reinterpret_cast<const uint2*>(dqkv + t * W + col);
+        v = make_float4(u16f<E>(x.x), u16f<E>(x.x >> 16), u16f<E>(x.y), u16f<E>(x.y >> 16));
+      } else {
+        v = *reinterpret_cast<const float4*>(dq_acc + t * Hq * D + col);
+      }
     } else {
       const bool isk = col < (Hq + Hkv) * D;
       const int c2 = col - (isk ? Hq * D : (Hq + Hkv) * D);
@@ -1372,6 +1405,18 @@ __global__ __launch_bounds__(256) void flash_bwd_finalize_kernel(
         v.x += u16f<E>(x.x); v.y += u16f<E>(x.x >> 16);
         v.z += u16f<E>(x.y); v.w += u16f<E>(x.y >> 16);
       }
+    }
+    if (cos_t != nullptr && col < (Hq + Hkv) * D) {
+      // two interleaved pairs (col, col + 1), (col + 2, col + 3) of one head
+      const int fi = (col % D) >> 1;
+      const long pos = t % S;
+      const float2 c = *reinterpret_cast<const float2*>(cos_t + pos * (D / 2) + fi);
+      const float2 sn = *reinterpret_cast<const float2*>(sin_t + pos * (D / 2) + fi);
+      const float a0 = v.x, b0 = v.y, a1 = v.z, b1 = v.w;
+      v.x = a0 * c.x + b0 * sn.x;
+      v.y = -a0 * sn.x + b0 * c.x;
+      v.z = a1 * c.y + b1 * sn.y;
+      v.w = -a1 * sn.y + b1 * c.y;
     }
     uint2 o;
     o.x = pk2<E>(v.x, v.y);
@@ -1496,9 +1541,16 @@ std::tuple<at::Tensor, at::Tensor> flash_fwd(const at::Tensor& qk, const at::Ten
 }
 
 // Returns dqkv [T, (Hq+2Hkv)*D] bf16 (dQ/dK in the rotated frame; RoPE backward follows).
+// rope.hip: in-place RoPE backward on the Q / K columns of dqkv
+void rope_bwd_(const at::Tensor& dqkv, const at::Tensor& cos_t, const at::Tensor& sin_t, int64_t seq_len,
+               int64_t hq, int64_t hkv, int64_t d);
+
+// cos / sin given: the returned dQ / dK are rotated back (the gradient of the UNROTATED
+// projection), inside the pass that folds the GQA dK / dV partials.
 at::Tensor flash_bwd(const at::Tensor& dout, const at::Tensor& qk, const at::Tensor& qkv,
                      const at::Tensor& out, const at::Tensor& lse, int64_t S, int64_t Hq,
-                     int64_t Hkv, int64_t D, int64_t mode) {
+                     int64_t Hkv, int64_t D, int64_t mode, const std::optional<at::Tensor>& cos_t,
+                     const std::optional<at::Tensor>& sin_t) {
   check_inputs(qk, qkv, S, Hq, Hkv, D);
   FT_CHECK_CONTIG(dout);
   FT_CHECK_CONTIG(out);
@@ -1526,6 +1578,16 @@ at::Tensor flash_bwd(const at::Tensor& dout, const at::Tensor& qk, const at::Ten
   bf16_t* dkp = direct ? mptr<bf16_t>(dqkv) + (long)Hq * D : mptr<bf16_t>(dk_part);
   bf16_t* dvp = direct ? mptr<bf16_t>(dqkv) + (long)(Hq + Hkv) * D : mptr<bf16_t>(dv_part);
   const long ldkv = direct ? (long)(Hq + 2 * Hkv) * D : (long)Hq * D;
+  const bool rope = cos_t.has_value() && cos_t->defined();
+  if (rope) {
+    TORCH_CHECK(sin_t.has_value() && sin_t->defined(), "flash_bwd: cos without sin");
+    FT_CHECK_F32((*cos_t));
+    FT_CHECK_F32((*sin_t));
+    FT_CHECK_CONTIG((*cos_t));
+    FT_CHECK_CONTIG((*sin_t));
+    TORCH_CHECK(cos_t->size(0) >= S && cos_t->size(1) == D / 2 && sin_t->sizes() == cos_t->sizes(),
+                "flash_bwd: rope tables must be [>= S, D / 2]");
+  }
   const float sl2 = LOG2E_F / std::sqrt((float)D);
   const float scale = 1.f / std::sqrt((float)D);
   const long ldqk = qk.size(-1);
@@ -1554,53 +1616,61 @@ at::Tensor flash_bwd(const at::Tensor& dout, const at::Tensor& qk, const at::Ten
   // 94 -> 83 us for the whole backward; 8B layer 173 -> 167 us; S = 16384 1006 -> 972 us
   // (profiles/r2_flash_key_split.log)
   const bool dq_split = g_dq_split != 0;
+  // deterministic mode: the dQ kernel runs first and forms delta itself (no flash_bwd_pre pass),
+  // then the dK / dV kernel reads it
 #define FT_DQ(DD, NW_)                                                                                  \
   if (dq_split)                                                                                         \
     hipLaunchKernelGGL((flash_bwd_dq_kernel<E, DD, NW_, 2>), grid2, dim3(128 * NW_), 0, ft_stream(),       \
                        cptr<bf16_t>(dout), cptr<bf16_t>(qk), cptr<bf16_t>(qkv), cptr<float>(lse),       \
-                       cptr<float>(delta), mptr<bf16_t>(dqkv), B, (int)S, (int)Hq, (int)Hkv, sl2, scale, ldqk); \
+                       mptr<float>(delta), mptr<bf16_t>(dqkv), B, (int)S, (int)Hq, (int)Hkv, sl2, scale, ldqk, \
+                       cptr<bf16_t>(out));                                                              \
   else                                                                                                  \
     hipLaunchKernelGGL((flash_bwd_dq_kernel<E, DD, NW_, 1>), grid2, block2, 0, ft_stream(),                \
                        cptr<bf16_t>(dout), cptr<bf16_t>(qk), cptr<bf16_t>(qkv), cptr<float>(lse),       \
-                       cptr<float>(delta), mptr<bf16_t>(dqkv), B, (int)S, (int)Hq, (int)Hkv, sl2, scale, ldqk)
+                       mptr<float>(delta), mptr<bf16_t>(dqkv), B, (int)S, (int)Hq, (int)Hkv, sl2, scale, ldqk, \
+                       cptr<bf16_t>(out))
+#define FT_PRE(DD)                                                                                      \
+  hipLaunchKernelGGL((flash_bwd_pre_kernel<E, DD>), dim3(pre_blocks), block, 0, ft_stream(),             \
+                     cptr<bf16_t>(dout), cptr<bf16_t>(out), mptr<float>(delta), B, (int)S, (int)Hq)
   FT_DISPATCH_E16(qk.scalar_type(), {
     if (D == 128) {
-      hipLaunchKernelGGL((flash_bwd_pre_kernel<E, 128>), dim3(pre_blocks), block, 0, ft_stream(),
-                         cptr<bf16_t>(dout), cptr<bf16_t>(out), mptr<float>(delta), B, (int)S, (int)Hq);
-      if (mode == 0) FT_BWD(128, 0);
-      else if (mode == 1) { if (g_dkdv2 && nw == 4) { FT_DKDV2(128, 4, 1); } else FT_BWD(128, 1); FT_DQ(128, 4); }
-      else FT_BWD(128, 2);
+      if (mode == 0) { FT_PRE(128); FT_BWD(128, 0); }
+      else if (mode == 1) { FT_DQ(128, 4); if (g_dkdv2 && nw == 4) { FT_DKDV2(128, 4, 1); } else FT_BWD(128, 1); }
+      else { FT_PRE(128); FT_BWD(128, 2); }
     } else {
-      hipLaunchKernelGGL((flash_bwd_pre_kernel<E, 64>), dim3(pre_blocks), block, 0, ft_stream(),
-                         cptr<bf16_t>(dout), cptr<bf16_t>(out), mptr<float>(delta), B, (int)S, (int)Hq);
-      if (mode == 0) FT_BWD(64, 0);
+      if (mode == 0) { FT_PRE(64); FT_BWD(64, 0); }
       else if (mode == 1 && nw == 2) {
-        if (kv_split) FT_DKDV2(64, 2, 2); else FT_DKDV2(64, 2, 1);
         FT_DQ(64, 2);
+        if (kv_split) FT_DKDV2(64, 2, 2); else FT_DKDV2(64, 2, 1);
       }
       // head_dim 64 with 4-wave blocks: the one-slice dK/dV kernel is faster (S = 8192, 16 heads:
       // 631 vs 783 us, profiles/r2_flash_long_context.log); FT_FLASH_DKDV2=2 forces the slice pair
       else if (mode == 1) {
+        FT_DQ(64, 4);
         if (g_dkdv2_64 && kv_split) FT_DKDV2(64, 4, 2);
         else if (g_dkdv2_64) FT_DKDV2(64, 4, 1);
         else FT_BWD(64, 1);
-        FT_DQ(64, 4);
       }
-      else FT_BWD(64, 2);
+      else { FT_PRE(64); FT_BWD(64, 2); }
     }
   });
 #undef FT_BWD
 #undef FT_DKDV2
 #undef FT_DQ
+#undef FT_PRE
   FT_LAUNCH_CHECK();
-  if (direct) return dqkv;
+  if (direct) {  // no GQA partials to fold: only the RoPE backward remains
+    if (rope) rope_bwd_(dqkv, *cos_t, *sin_t, S, Hq, Hkv, D);
+    return dqkv;
+  }
   const long vec = (long)T * ((Hq + 2 * Hkv) * D / 4);
   const int fin_blocks = (int)std::max(1L, std::min((vec + 255) / 256, 4096L));
   FT_DISPATCH_E16(qk.scalar_type(),
                   hipLaunchKernelGGL((flash_bwd_finalize_kernel<E>), dim3(fin_blocks), block, 0, ft_stream(),
                                      det ? nullptr : cptr<float>(dq_acc), cptr<bf16_t>(dk_part),
                                      cptr<bf16_t>(dv_part), mptr<bf16_t>(dqkv), (long)T, (int)Hq,
-                                     (int)Hkv, (int)D));
+                                     (int)Hkv, (int)D, rope ? cptr<float>(*cos_t) : nullptr,
+                                     rope ? cptr<float>(*sin_t) : nullptr, (int)S));
   FT_LAUNCH_CHECK();
   return dqkv;
 }
@@ -1623,6 +1693,6 @@ TORCH_LIBRARY_FRAGMENT(ftamd, m) {
         &flash_fwd);
   m.def(
       "flash_bwd(Tensor dout, Tensor qk, Tensor qkv, Tensor out, Tensor lse, int S, int Hq, int "
-      "Hkv, int D, int mode=0) -> Tensor",
+      "Hkv, int D, int mode=0, Tensor? cos=None, Tensor? sin=None) -> Tensor",
       &flash_bwd);
 }

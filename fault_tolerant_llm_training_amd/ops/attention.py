@@ -40,9 +40,15 @@ def flash_attn_fwd(qk, qkv, S, hq, hkv, d):
     return tuple(kernels().flash_fwd(qk, qkv, S, hq, hkv, d))
 
 
-def flash_attn_bwd(do, qk, qkv, o, lse, S, hq, hkv, d):
-    """Returns dqkv [T, (Hq+2Hkv)*D] with dQ/dK still in the rotated frame. Both variants are
-    deterministic (fp32: always; bf16 / fp16: unless FT_FLASH_BWD_MODE=0)."""
+def flash_attn_bwd(do, qk, qkv, o, lse, S, hq, hkv, d, cos=None, sin=None):
+    """Returns dqkv [T, (Hq+2Hkv)*D]. With ``cos`` / ``sin`` the dQ / dK columns are rotated back
+    (RoPE backward, reference model.py:100-126): the gradient of the UNROTATED projection — on the
+    16-bit path inside the kernel pass that folds the GQA dK / dV partials (no separate RoPE
+    pass); without them dQ / dK stay in the rotated frame. Both variants are deterministic (fp32:
+    always; bf16 / fp16: unless FT_FLASH_BWD_MODE=0)."""
     if qk.dtype == torch.float32:
-        return kernels().flash_f32_bwd(do, qk, qkv, o, lse, S, hq, hkv, d)
-    return kernels().flash_bwd(do, qk, qkv, o, lse, S, hq, hkv, d, _BWD_MODE)
+        dqkv = kernels().flash_f32_bwd(do, qk, qkv, o, lse, S, hq, hkv, d)
+        if cos is not None:
+            kernels().rope_bwd_(dqkv, cos, sin, S, hq, hkv, d)
+        return dqkv
+    return kernels().flash_bwd(do, qk, qkv, o, lse, S, hq, hkv, d, _BWD_MODE, cos, sin)

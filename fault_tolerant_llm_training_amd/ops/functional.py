@@ -613,8 +613,9 @@ class AttentionKeep:
 class RopeAttentionFn(torch.autograd.Function):
     """RoPE + causal GQA attention on the packed projection. ``rotated``: Q/K of ``qkv`` were
     already rotated by the QKV projection's epilogue (:class:`QKVRopeFn`, GPU only): the flash
-    kernels then read Q/K straight from ``qkv`` and the gradient is returned in the rotated frame
-    (the projection's backward rotates it back)."""
+    kernels then read Q/K straight from ``qkv``. Either way backward returns the gradient of the
+    UNROTATED projection: the flash backward rotates dQ/dK back in the pass that folds the GQA
+    dK/dV partials (so neither this node nor the projection's backward runs a RoPE pass)."""
 
     @staticmethod
     def forward(ctx, qkv, cos, sin, seq_len, hq, hkv, d, keep=None, gen=-1, rotated=False):
@@ -652,9 +653,7 @@ class RopeAttentionFn(torch.autograd.Function):
             from .attention import flash_attn_bwd
 
             qkv, qk, o, lse, cos, sin = ctx.saved_tensors
-            dqkv = flash_attn_bwd(do.contiguous(), qk, qkv, o, lse, seq_len, hq, hkv, d)
-            if not ctx.rotated:
-                kernels().rope_bwd_(dqkv, cos, sin, seq_len, hq, hkv, d)
+            dqkv = flash_attn_bwd(do.contiguous(), qk, qkv, o, lse, seq_len, hq, hkv, d, cos, sin)
             return dqkv, None, None, None, None, None, None, None, None, None
         qkv, cos, sin = ctx.saved_tensors
         with torch.enable_grad():
@@ -697,7 +696,8 @@ def _qkv_rope_ok(x2: torch.Tensor, w: torch.Tensor, d: int) -> bool:
 
 class QKVRopeFn(torch.autograd.Function):
     """qkv = x W^T with Q/K rotated (reference model.py:195 then :100-126). Backward receives the
-    gradient in the rotated frame, rotates it back in place (rope_bwd_), then dW / dX."""
+    gradient of the unrotated projection (the attention backward already rotated dQ/dK back,
+    :class:`RopeAttentionFn`), then dW / dX."""
 
     @staticmethod
     def forward(ctx, x2, w, sink, cos, sin, seq_len, hq, hkv, d):
@@ -711,7 +711,6 @@ class QKVRopeFn(torch.autograd.Function):
         x2, w, cos, sin = ctx.saved_tensors
         seq_len, hq, hkv, d = ctx.cfg
         dq = dq.contiguous()
-        kernels().rope_bwd_(dq, cos, sin, seq_len, hq, hkv, d)
         dw = weight_grad_async(dq, x2, ctx.sink)
         dx = mm_dx(dq, w)
         return dx, dw, None, None, None, None, None, None, None

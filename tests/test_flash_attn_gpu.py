@@ -221,3 +221,29 @@ def test_flash_dkdv_split_matches(B, S, Hq, Hkv, D):
     nq = Hq * D
     assert torch.equal(g1[:, :nq], g0[:, :nq])  # dQ untouched
     assert rel(g1[:, nq:], g0[:, nq:]) < 4e-3
+
+
+@pytest.mark.parametrize("B,S,Hq,Hkv,D,mode", [(1, 2048, 32, 8, 128, 1), (1, 512, 8, 2, 64, 1), (2, 256, 4, 4, 64, 1),
+                                              (1, 1000, 4, 2, 128, 0), (2, 512, 12, 12, 64, 1)])
+def test_flash_bwd_with_rope_backward(B, S, Hq, Hkv, D, mode):
+    """flash_bwd(..., cos, sin): the gradient of the UNROTATED projection, the RoPE backward done
+    in the pass that folds the GQA partials (or by rope_bwd_ when there is nothing to fold) ==
+    flash_bwd then rope_bwd_ (reference model.py:100-126) within one bf16 rounding; deterministic."""
+    from fault_tolerant_llm_training_amd._native import kernels
+    from fault_tolerant_llm_training_amd.models.llama import rope_tables
+
+    K = kernels()
+    torch.manual_seed(2)
+    T = B * S
+    qkv = torch.randn(T, (Hq + 2 * Hkv) * D, device="cuda").bfloat16()
+    qk = torch.randn(T, (Hq + Hkv) * D, device="cuda").bfloat16()
+    do = torch.randn(T, Hq * D, device="cuda").bfloat16()
+    cos, sin = (t.cuda() for t in rope_tables(D, S, 500000.0))
+    o, lse = K.flash_fwd(qk, qkv, S, Hq, Hkv, D)
+    ref = K.flash_bwd(do, qk, qkv, o, lse, S, Hq, Hkv, D, mode)
+    K.rope_bwd_(ref, cos, sin, S, Hq, Hkv, D)
+    got = K.flash_bwd(do, qk, qkv, o, lse, S, Hq, Hkv, D, mode, cos, sin)
+    for lo, hi in ((0, Hq * D), (Hq * D, (Hq + Hkv) * D), ((Hq + Hkv) * D, (Hq + 2 * Hkv) * D)):
+        assert rel(got[:, lo:hi], ref[:, lo:hi]) < 4e-3, (lo, hi)
+    if mode == 1:
+        assert torch.equal(got, K.flash_bwd(do, qk, qkv, o, lse, S, Hq, Hkv, D, mode, cos, sin))
