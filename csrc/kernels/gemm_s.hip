@@ -65,7 +65,7 @@ __device__ __forceinline__ void dma16(const i32x4_t& srd, unsigned voff, unsigne
   asm volatile("s_add_u32 m0, %2, %4\n\tbuffer_load_dwordx4 %0, %1, %3 offen lds"
                :
                : "v"(voff), "s"(srd), "s"(sbase), "s"(soff), "i"(IMM)
-               : "memory");
+               : "memory", "scc");
 }
 
 template <int OFF>

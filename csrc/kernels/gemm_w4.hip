@@ -91,13 +91,14 @@ __device__ __forceinline__ i32x4_t make_srd(const void* p) {
 
 // LDS-DMA, 2 instructions: 16 B per lane from srd + voff + soff into LDS [m0 + 16 * lane],
 // m0 = sbase + IMM. m0 is used by nothing else in this kernel (no LDS-DMA builtins, no GDS), so it
-// is not saved; gfx950 needs no wait state between the m0 write and the DMA.
+// is not saved; gfx950 needs no wait state between the m0 write and the DMA. s_add_u32 writes SCC:
+// declared, else the scheduler may put the K loop's compare before a DMA and branch on the carry.
 template <int IMM>
 __device__ __forceinline__ void dma16(const i32x4_t& srd, unsigned voff, unsigned soff, unsigned sbase) {
   asm volatile("s_add_u32 m0, %2, %4\n\tbuffer_load_dwordx4 %0, %1, %3 offen lds"
                :
                : "v"(voff), "s"(srd), "s"(sbase), "s"(soff), "i"(IMM)
-               : "memory");
+               : "memory", "scc");
 }
 
 template <int OFF>
@@ -202,11 +203,42 @@ __device__ __forceinline__ int2 tile_of(int bid, int tiles_m, int tiles_n, int n
   return nfast ? make_int2(w / tiles_n, w % tiles_n) : make_int2(w % tiles_m, w / tiles_m);
 }
 
+// the accumulators "written" by an empty asm: a point the register allocator's copies and
+// materialisations of them cannot cross (see the uses)
+template <int NJ>
+__device__ __forceinline__ void tie_acc(f32x4_t (&acc)[8][NJ]) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) asm volatile("" : "+a"(acc[i][j]));
+}
+
 template <int NJ, bool AT, bool BT>
 struct Frags {
   Frag<AT> a0[8], a1[8];
   Frag<BT> b0[NJ], b1[NJ];
 };
+
+__device__ __forceinline__ void tie_frag(Frag<false>& x) { asm volatile("" : "+v"(x.v)); }
+__device__ __forceinline__ void tie_frag(Frag<true>& x) { asm volatile("" : "+v"(x.lo), "+v"(x.hi)); }
+
+// every fragment register "written" here: the asm LDS reads are asynchronous, but the compiler
+// takes their outputs as complete at the asm, so it may hand a register whose read is still in
+// flight (the dead next-k-step reads of the last K-tile) to other code; a tie placed after the
+// lgkmcnt(0) wait keeps all of them reserved until the reads have landed
+template <int NJ, bool AT, bool BT>
+__device__ __forceinline__ void tie_frags(Frags<NJ, AT, BT>& f) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    tie_frag(f.a0[i]);
+    tie_frag(f.a1[i]);
+  }
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    tie_frag(f.b0[j]);
+    tie_frag(f.b1[j]);
+  }
+}
 
 template <int NJ, bool AT, bool BT>
 struct Sched {
@@ -292,12 +324,14 @@ __device__ __forceinline__ void rd_slot(Frag<AT> (&ax)[8], Frag<BT> (&bx)[NJ], c
   });
 }
 
-// One K-tile t in stage CUR = t & 1: DMA: stage tile t + 2 into this stage; NEXT: read tile t + 1's
-// first k-step (stage 1 - CUR).
+// One K-tile t in stage CUR = t & 1: DMA: stage tile t + 2 into this stage (clamped to the last
+// tile: the last two K-tiles re-stage it into a stage nobody reads again); NEXT: read tile t + 1's
+// first k-step (stage 1 - CUR; after the last tile these reads are dead).
 template <class E, int NJ, bool AT, bool BT, int CUR, bool DMA, bool NEXT>
-__device__ __forceinline__ void ktile(f32x4_t (&acc)[8][NJ], Frags<NJ, AT, BT>& f, int t, const Ctx& c) {
+__device__ __forceinline__ void ktile(f32x4_t (&acc)[8][NJ], Frags<NJ, AT, BT>& f, int t, int nk, const Ctx& c) {
   using S = Sched<NJ, AT, BT>;
-  const unsigned kofsA = (unsigned)(t + 2) * c.stepA, kofsB = (unsigned)(t + 2) * c.stepB;
+  const int tn2 = __builtin_amdgcn_readfirstlane(min(t + 2, nk - 1));
+  const unsigned kofsA = (unsigned)tn2 * c.stepA, kofsB = (unsigned)tn2 * c.stepB;
   const unsigned sb = c.sbase;
   sfor<2 * S::MH>([&](auto SS) {
     constexpr int s = SS;
@@ -454,30 +488,41 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(W4Args p) {
   barrier();
   sfor<S::R>([&](auto RR) { rd<NJ, AT, BT, 0, 0, RR>(f.a0, f.b0, c); });
 
-  // the zeroed accumulators are MFMA sources next (VALU write -> MFMA SrcC wait states)
+  // the zeroed accumulators are MFMA sources next (VALU write -> MFMA SrcC wait states): the
+  // ties pin every zero write before the pad (the register allocator places copies and
+  // materialisations freely; an asm that "writes" the accumulators is a fence it cannot cross)
+  tie_acc(acc);
   __builtin_amdgcn_sched_barrier(0);
   asm volatile("s_nop 4" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
-  // nk is even (K % 128, checked on the host): K-tiles 0 .. nk - 3 stage tile t + 2, unrolled by
-  // two so every stage offset is static; the last two read what is already staged. (No runtime
-  // branch between alternative tails: with the accumulators live across one the register
-  // allocator spilled them.)
+  // nk is even (K % 128, checked on the host): K-tiles in pairs so every stage offset is static,
+  // and ONE code path for every tile (the last two re-stage the last tile and read a dead next
+  // k-step): with a separate tail the register allocator placed the accumulators differently in
+  // the tail and copied them across with v_accvgpr_mov right behind the asm MFMAs that were still
+  // writing them (the compiler cannot see those as MFMAs) -> stale accumulators.
   int t = 0;
-  for (; t + 2 < nk; t += 2) {
-    ktile<E, NJ, AT, BT, 0, true, true>(acc, f, t, c);
-    ktile<E, NJ, AT, BT, 1, true, true>(acc, f, t + 1, c);
-  }
-  ktile<E, NJ, AT, BT, 0, false, true>(acc, f, t, c);
-  ktile<E, NJ, AT, BT, 1, false, false>(acc, f, t + 1, c);
-  // The accumulators are read by VALU next: wait out the last MFMAs (the compiler does not see
-  // the asm as MFMAs, so it inserts no wait states), and keep every accumulator read behind the
-  // pad (sched_barrier: register-only instructions may otherwise be hoisted above an asm).
+  do {
+    ktile<E, NJ, AT, BT, 0, true, true>(acc, f, t, nk, c);
+    ktile<E, NJ, AT, BT, 1, true, true>(acc, f, t + 1, nk, c);
+    t += 2;
+  } while (t < nk);
+  // Drain: the re-staging DMAs of the last two K-tiles and the dead next-k-step reads land, and
+  // the last MFMAs finish before VALU reads the accumulators (the compiler does not see the asm
+  // as MFMAs, so it inserts no wait states; sched_barrier: register-only instructions may
+  // otherwise be hoisted above an asm).
   __builtin_amdgcn_sched_barrier(0);
-  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
+  // ... and the ties: the accumulators and fragments are (as far as the compiler knows) produced
+  // here, so no read or copy of an accumulator, and no reuse of a fragment register, can be
+  // placed above the drain (both happened at the loop exit without them: accumulators copied
+  // right behind the asm MFMAs still writing them; index math written into registers whose
+  // dead LDS reads had not returned yet)
+  tie_frags(f);
+  tie_acc(acc);
 
   // ---- epilogue through LDS: quadrant rows of 256 B (NW * 2 used), chunk c at c ^ (row & 15)
-  barrier();  // every wave's last fragment reads are done (no DMA is in flight)
+  barrier();  // every wave is done with the stages before they become epilogue staging
   char* wl = smem + wid * 32768;
   {
     const int lr = lane & 15, hc = lane >> 4;  // acc row, 4-column group of the fragment

@@ -1027,8 +1027,11 @@ def set_w4_head(on: bool) -> None:
     _W4_HEAD = bool(on)
 
 
+_W4_HEAD_MIN_K = 2048  # model dim from which the head's logits go to w4 (GPT-2 sizes: hipBLASLt)
+
+
 def _head_fwd(h2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
-    if _W4_HEAD and _W4_FWD and _w4_fits(h2, w) and h2.is_contiguous():
+    if _W4_HEAD and _W4_FWD and h2.shape[1] >= _W4_HEAD_MIN_K and _w4_fits(h2, w) and h2.is_contiguous():
         return kernels().gemm_nt_w4(h2, w, None, None, 0)
     return mm_fwd(h2, w)
 
