@@ -305,6 +305,8 @@ _DW_STREAM = os.environ.get("FT_DW_STREAM", "1") == "1"
 _dw_streams = {}
 _dw_pending = {}  # device -> FIFO of (dW done event, operands kept alive until then)
 _DW_LAG = int(os.environ.get("FT_DW_LAG", "4"))  # dW GEMMs the compute stream may run ahead by
+# dW GEMMs that take the w4 kernel on k-major operands run inline unless FT_W4_DW_SIDE=1
+_W4_DW_SIDE = os.environ.get("FT_W4_DW_SIDE", "0") == "1"
 
 
 def set_dw_stream(on: bool) -> None:
@@ -343,6 +345,11 @@ def weight_grad_async(dy2: torch.Tensor, x2: Optional[torch.Tensor], sink: Optio
     xx = x2 if x2 is not None else xT.t()
     bufs = None
     w4t = dyT is None and xT is None and _w4t_fits(dy2.shape[1], xx.shape[1], dy2.shape[0], dy2, xx)
+    if w4t and not _W4_DW_SIDE:
+        # the w4 kernels hold one workgroup per CU: a concurrent dX kernel cannot co-reside, so the
+        # side stream only adds cross-stream waits (8B step 108.5 -> 106.9 ms with dW inline,
+        # profiles/r4_ab.log)
+        return weight_grad(dy2, x2, sink, dyT, xT)
     if not w4t and _use_tn(dy2, xx) and not _hand("dw", dy2.shape[1], xx.shape[1], dy2.shape[0], dy2, xx):
         T, N = dy2.shape
         bufs = (dy2.new_empty((N, T)) if dyT is None else None,

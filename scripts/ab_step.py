@@ -24,6 +24,7 @@ Knobs toggled between timing windows (alternating rounds, so box and clock drift
   psums — the gradient-norm partials written by the dW / norm epilogues instead of a sumsq pass
   w4head — the LM-head logits GEMM on the w4 kernel
   r4    — w4bwd + psums + w4head together (round-4 routing vs round-3)
+  w4dwside — the w4 weight gradients on the dW side stream (default: inline on the compute stream)
 Usage: python scripts/ab_step.py [--steps 8] [--rounds 3] [--configs gemm,dw ...]
 """
 from __future__ import annotations
@@ -129,6 +130,7 @@ def main():
                "w4bwd": lambda on: (torch.cuda.synchronize(), Fx.set_w4_bwd(on)),
                "psums": lambda on: (torch.cuda.synchronize(), red.set_producer_sums(on)),
                "w4head": lambda on: (torch.cuda.synchronize(), Fx.set_w4_head(on)),
+               "w4dwside": lambda on: (torch.cuda.synchronize(), setattr(Fx, "_W4_DW_SIDE", on)),
                "r4": lambda on: (torch.cuda.synchronize(), Fx.set_w4_bwd(on), red.set_producer_sums(on),
                                  Fx.set_w4_head(on)),
                "w4wide": lambda on: (torch.cuda.synchronize(), setattr(Fx, "_W4_FWD_MAX_NJ", 8 if on else 6))}
