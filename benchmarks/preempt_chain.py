@@ -24,6 +24,7 @@ from datetime import datetime
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
+from fault_tolerant_llm_training_amd.ckpt.format import checkpoint_file  # noqa: E402
 from fault_tolerant_llm_training_amd.ft.slurm_sim import SlurmSim  # noqa: E402
 
 TS = re.compile(r"^(\d{4}-\d\d-\d\d \d\d:\d\d:\d\d,\d{3}) - ")
@@ -74,6 +75,9 @@ def main():
     ap.add_argument("--signal-lead", type=float, default=30.0)
     ap.add_argument("--workdir", default=ROOT)
     ap.add_argument("--checkpoint-path", default="")
+    ap.add_argument("--prune-consumed", action="store_true",
+                    help="delete a job's checkpoint once the next job has resumed from it (an 8B chain "
+                         "holds one 48 GB checkpoint on disk at a time instead of one per job)")
     ap.add_argument("train_args", nargs=argparse.REMAINDER)
     a = ap.parse_args()
     extra = [x for x in a.train_args if x != "--"]
@@ -85,7 +89,25 @@ def main():
     logdir = tempfile.mkdtemp(prefix="ftlogs_")
     sim = SlurmSim(a.workdir, a.time, a.signal_lead, kill_wait=30.0, env=env, log_dir=logdir)
     sim.submit("train.sh")
-    jobs = sim.run(a.jobs)
+    pruned = []
+
+    def prune(rec):
+        # the running job has loaded its predecessor's checkpoint: that file is no longer needed
+        if not sim.jobs or sim.jobs[-1].job_id in pruned:
+            return
+        prev = sim.jobs[-1].job_id
+        try:
+            with open(rec.log) as f:
+                resumed = "Resuming training from training_step" in f.read()
+        except OSError:
+            return
+        if resumed:
+            path = checkpoint_file(ck, prev)
+            if os.path.exists(path):
+                os.remove(path)
+            pruned.append(prev)
+
+    jobs = sim.run(a.jobs, prune if a.prune_consumed else None)
     rows, lost = [], 0
     prev = None
     for j in jobs:
@@ -97,6 +119,7 @@ def main():
         prev = r
     print(json.dumps({"benchmark": "preempt_chain", "args": extra, "time_limit_s": a.time,
                       "signal_lead_s": a.signal_lead, "jobs": rows, "steps_lost": lost,
+                      "pruned_checkpoints": pruned,
                       "logs": logdir}), flush=True)
     return 0
 

@@ -109,7 +109,8 @@ class SlurmSim:
         except ProcessLookupError:
             pass
 
-    def run_job(self, req: dict) -> JobRecord:
+    def run_job(self, req: dict, hook=None) -> JobRecord:
+        """Runs one queued job to its end; ``hook(rec)`` is called every poll (50 ms) while it runs."""
         jid, argv = req["id"], req["argv"]
         rec = JobRecord(jid, argv, log=os.path.join(self.log_dir, f"output_{jid}.out"))
         env = dict(self.env)
@@ -133,18 +134,20 @@ class SlurmSim:
                 elif stage == 2 and el >= self.time_limit + self.kill_wait:
                     self._signal(p, signal.SIGKILL, rec)
                     stage = 3
+                if hook is not None:
+                    hook(rec)
                 time.sleep(0.05)
         rec.returncode = p.returncode
         rec.seconds = time.monotonic() - t0
         self.jobs.append(rec)
         return rec
 
-    def run(self, max_jobs: int = 10) -> List[JobRecord]:
+    def run(self, max_jobs: int = 10, hook=None) -> List[JobRecord]:
         while len(self.jobs) < max_jobs:
             req = self._pop()
             if req is None:
                 break
-            self.run_job(req)
+            self.run_job(req, hook)
         return self.jobs
 
 

@@ -42,3 +42,25 @@ def test_usr1_resubmit_chain_x3(tmp_path):
             assert f"Resuming training from training_step {prev_saved}" in out, out
             assert saved > prev_saved
         prev_saved = saved
+
+
+def test_preempt_chain_prunes_consumed_checkpoints(tmp_path):
+    """benchmarks/preempt_chain.py --prune-consumed (the 8B chain on a 79 GB disk): each job's
+    checkpoint is deleted once the next job has resumed from it; zero steps lost still holds."""
+    import json
+    import subprocess
+    import sys
+
+    ck = tmp_path / "ck"
+    env = dict(os.environ, OMP_NUM_THREADS="2", PYTHONUNBUFFERED="1")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "benchmarks", "preempt_chain.py"), "--jobs", "3",
+                        "--time", "14", "--signal-lead", "7", "--checkpoint-path", str(ck), "--prune-consumed", "--",
+                        "--device", "cpu", "--model", "tiny", "--synthetic-data", "--vocab-size", "256",
+                        "--sequence-length", "32", "--logging-frequency", "50"],
+                       env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    ids = [j["job"] for j in res["jobs"]]
+    assert res["steps_lost"] == 0 and all(j["saved_at"] for j in res["jobs"]), res
+    assert res["pruned_checkpoints"] == ids[:2], res
+    assert sorted(os.listdir(ck)) == [f"checkpoint_{ids[2]}.ckpt"]
