@@ -75,6 +75,7 @@ def main():
     ap.add_argument("--signal-lead", type=float, default=30.0)
     ap.add_argument("--workdir", default=ROOT)
     ap.add_argument("--checkpoint-path", default="")
+    ap.add_argument("--log-dir", default="", help="where the jobs' output_<JOBID>.out go (default: a temp dir)")
     ap.add_argument("--prune-consumed", action="store_true",
                     help="delete a job's checkpoint once the next job has resumed from it (an 8B chain "
                          "holds one 48 GB checkpoint on disk at a time instead of one per job)")
@@ -86,7 +87,8 @@ def main():
     env["EXTRA_TRAINING_ARGS"] = " ".join(extra + ["--training-steps", "100000000", "--error-step", "100000000",
                                                    "--checkpoint-path", ck])
     env.setdefault("PYTHONUNBUFFERED", "1")
-    logdir = tempfile.mkdtemp(prefix="ftlogs_")
+    logdir = a.log_dir or tempfile.mkdtemp(prefix="ftlogs_")
+    os.makedirs(logdir, exist_ok=True)
     sim = SlurmSim(a.workdir, a.time, a.signal_lead, kill_wait=30.0, env=env, log_dir=logdir)
     sim.submit("train.sh")
     pruned = []

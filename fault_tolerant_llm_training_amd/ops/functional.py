@@ -195,11 +195,27 @@ def _w4t_fits(M: int, N: int, K: int, *ts) -> bool:
     return 0 < nj and (M // 256) * (N // (32 * nj)) >= _W4_MIN_TILES
 
 
+# dX products with a deep reduction (N >= FT_W4_DX_DEEP_K, default 16384: the 8B w13 dX, N = 2F =
+# 28672, and the LM-head dX, N = V) that fill the chip in one round of narrow tiles stay on
+# hipBLASLt: with 256 x 128 tiles the w4 loop is LDS-bound (48 KB of DMA + 96 KB of fragment reads
+# per K-tile per CU for 32 MFMAs per wave), 0.88-0.90x of hipBLASLt on the row-major operands
+# (profiles/r4_gemm_w4t_bench.log); the wider tiles leave half the CUs idle.
+_W4_DX_DEEP_K = int(os.environ.get("FT_W4_DX_DEEP_K", "16384"))
+
+
+def _w4_dx_ok(T: int, K: int, N: int, dy2: torch.Tensor, w: torch.Tensor) -> bool:
+    if not (_w4t_fits(T, K, N, dy2, w) and w.is_contiguous()):
+        return False
+    if N >= _W4_DX_DEEP_K and (T // 256) * (K // 256) <= 256:
+        return False
+    return True
+
+
 def mm_dx(dy2: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """dx = dy2 @ w: dy2 [T, N], w [N, K]."""
     T, N = dy2.shape
     K = w.shape[1]
-    if _w4t_fits(T, K, N, dy2, w) and w.is_contiguous():
+    if _w4_dx_ok(T, K, N, dy2, w):
         return kernels().gemm_w4_ex(dy2.contiguous(), False, w, True, T, K, N, out, False, None, 0)
     if out is not None:
         if _hand("dx", T, K, N, dy2, w):
@@ -985,7 +1001,7 @@ def _dx_into(out: torch.Tensor, dy2: torch.Tensor, w: torch.Tensor) -> None:
     """out[T, K] = dy2[T, N] @ w[N, K]."""
     T, N = dy2.shape
     K = w.shape[1]
-    if _w4t_fits(T, K, N, dy2, w) and out.is_contiguous() and w.is_contiguous():
+    if _w4_dx_ok(T, K, N, dy2, w) and out.is_contiguous():
         kernels().gemm_w4_ex(dy2, False, w, True, T, K, N, out, False, None, 0)
         return
     if _hand("dx", T, K, N, dy2, w):

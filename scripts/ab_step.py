@@ -24,6 +24,7 @@ Knobs toggled between timing windows (alternating rounds, so box and clock drift
   psums — the gradient-norm partials written by the dW / norm epilogues instead of a sumsq pass
   w4head — the LM-head logits GEMM on the w4 kernel
   r4    — w4bwd + psums + w4head together (round-4 routing vs round-3)
+  deepdx — the deep-reduction dX products (8B w13 dX, LM-head dX) on hipBLASLt instead of the w4 kernel
   w4dwside — the w4 weight gradients on the dW side stream (default: inline on the compute stream)
 Usage: python scripts/ab_step.py [--steps 8] [--rounds 3] [--configs gemm,dw ...]
 """
@@ -130,6 +131,7 @@ def main():
                "w4bwd": lambda on: (torch.cuda.synchronize(), Fx.set_w4_bwd(on)),
                "psums": lambda on: (torch.cuda.synchronize(), red.set_producer_sums(on)),
                "w4head": lambda on: (torch.cuda.synchronize(), Fx.set_w4_head(on)),
+               "deepdx": lambda on: (torch.cuda.synchronize(), setattr(Fx, "_W4_DX_DEEP_K", 16384 if on else 1 << 40)),
                "w4dwside": lambda on: (torch.cuda.synchronize(), setattr(Fx, "_W4_DW_SIDE", on)),
                "r4": lambda on: (torch.cuda.synchronize(), Fx.set_w4_bwd(on), red.set_producer_sums(on),
                                  Fx.set_w4_head(on)),
