@@ -304,9 +304,22 @@ def train(args) -> int:
             g["lr"] = lr
         logger.info("LR Scheduler loaded from checkpoint")
         restore_rng(checkpoint.get("rng"), device)
+    def log_digest(step: int, when: str = "") -> None:
+        """--state-digest: an order-independent digest of params / moments + the loader position,
+        comparable across a save (exit handler) and the resume from it, or across two runs."""
+        if not getattr(args, "state_digest", False):
+            return
+        from .utils.digest import state_digest
+
+        dg = state_digest(model.flat.params, optimizer.exp_avg, optimizer.exp_avg_sq)
+        logger.info(f"[rank {info.rank}] State digest at step {step}{when}: params={dg['params']} "
+                    f"exp_avg={dg['exp_avg']} exp_avg_sq={dg['exp_avg_sq']} "
+                    f"optimizer_step={optimizer.step_count} data_loader={json.dumps(loader.state_dict(), sort_keys=True)}")
+
     if checkpoint is not None:
         training_step = int(checkpoint["training_step"])
         logger.info(f"Resuming training from training_step {training_step}")
+        log_digest(training_step, " (resumed)")
     else:
         training_step = 0
         logger.info("Starting training!")
@@ -643,13 +656,7 @@ def train(args) -> int:
         boundary(final=True)  # drains the loss log, last non-finite check, last signals
         if ckpt["engine"] is not None:
             ckpt["engine"].wait()
-        if getattr(args, "state_digest", False):
-            from .utils.digest import state_digest
-
-            dg = state_digest(model.flat.params, optimizer.exp_avg, optimizer.exp_avg_sq)
-            logger.info(f"[rank {info.rank}] State digest at step {training_step}: params={dg['params']} "
-                        f"exp_avg={dg['exp_avg']} exp_avg_sq={dg['exp_avg_sq']} "
-                        f"optimizer_step={optimizer.step_count} data_loader={json.dumps(loader.state_dict(), sort_keys=True)}")
+        log_digest(training_step)
         logger.info("Training completed")
     except _StopTraining as stop:
         e = stop.cause
@@ -667,6 +674,7 @@ def train(args) -> int:
             if st is not None:
                 logger.info(f"Checkpoint {st.path}: {st.bytes / 1e9:.2f} GB in {st.total_s:.2f}s "
                             f"(mode {st.mode})")
+                log_digest(step_now, " (saved)")
 
         if exit_type == -1 and not isinstance(e, InjectedFault) and info.is_main:
             logger.error(f"Training error: {e!r}")

@@ -19,6 +19,9 @@ step r4_tests 400 python -u -m pytest -q --timeout 120 --timeout-method thread t
 step r4_gemm_bench 200 python -u scripts/gemm_w4t_bench.py
 step r4_ab 600 python -u scripts/ab_step.py --knobs ${AB_KNOBS:-r4,dw} --rounds 2 --steps 8
 step r4_bench 300 python -u bench.py --steps 20 --warmup 3 --no-ckpt
+if [ -n "$PROF" ]; then  # per-kernel stats of the default 8B step (rocprofv3 kernel trace only)
+  step r4_prof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_r4 -o run -- python3 bench.py --steps 5 --warmup 3 --no-ckpt
+fi
 if [ -n "$GPT2" ]; then
   step r4_gpt2_on 200 python -u bench.py --model gpt2-small --graph --steps 30 --warmup 5 --no-ckpt
   FT_W4_BWD=0 step r4_gpt2_off 200 python -u bench.py --model gpt2-small --graph --steps 30 --warmup 5 --no-ckpt

@@ -170,8 +170,13 @@ def test_state_digest_resume_equivalence_iterable(tmp_path):
     ref = _digest(out)
     rc, out = run_train(d, "41", base + ["--raise-error", "--error-step", "6"])
     assert rc == 0 and "Checkpoint saved at step 6" in out
+    saved = re.search(r"State digest at step 6 \(saved\): (.*)", out)
+    assert saved, out[-3000:]
     rc, out = run_train(d, "42", base + ["--checkpoint-id", "41"])
     assert rc == 0 and "Resuming training from training_step 6" in out, out[-3000:]
+    # the state the exit handler saved is the state the next job resumes from, bit for bit
+    resumed = re.search(r"State digest at step 6 \(resumed\): (.*)", out)
+    assert resumed and resumed.group(1).strip() == saved.group(1).strip(), (saved, resumed)
     assert _digest(out) == ref and ref[0] == 11
     rc, out = run_train(d, "43", base + ["--seed", "99"])
     assert rc == 0 and _digest(out)[1] != ref[1]
