@@ -33,6 +33,8 @@
 #include "torch_utils.h"
 
 #include <cstdlib>
+#include <map>
+#include <mutex>
 #include <string>
 #include <type_traits>
 #include <utility>
@@ -931,6 +933,157 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_kernel(
     }
 }
 
+// One 4-column unit (row t, columns col .. col + 3) of the GQA fold / RoPE backward into dqkv
+// (see flash_bwd_finalize_kernel): dQ from dq_acc (fp32) or rotated in place, dK / dV summed over
+// the G q-head partials in head order (the same order wherever it runs: bit-reproducible).
+template <class E>
+__device__ __forceinline__ void fin_unit(const float* __restrict__ dq_acc, const bf16_t* __restrict__ dk_part,
+                                         const bf16_t* __restrict__ dv_part, bf16_t* __restrict__ dqkv, long t,
+                                         int col, int Hq, int Hkv, int D, const float* __restrict__ cos_t,
+                                         const float* __restrict__ sin_t, int S) {
+  const int G = Hq / Hkv;
+  const int W = (Hq + 2 * Hkv) * D;
+  float4 v;
+  if (col < Hq * D) {
+    if (dq_acc == nullptr) {  // dQ already written by the deterministic dQ kernel
+      if (cos_t == nullptr) return;
+      const uint2 x = *reinterpret_cast<const uint2*>(dqkv + t * W + col);
+      v = make_float4(u16f<E>(x.x), u16f<E>(x.x >> 16), u16f<E>(x.y), u16f<E>(x.y >> 16));
+    } else {
+      v = *reinterpret_cast<const float4*>(dq_acc + t * Hq * D + col);
+    }
+  } else {
+    const bool isk = col < (Hq + Hkv) * D;
+    const int c2 = col - (isk ? Hq * D : (Hq + Hkv) * D);
+    const int kh = c2 / D, d = c2 % D;
+    const bf16_t* src = (isk ? dk_part : dv_part) + t * Hq * D + (long)kh * G * D + d;
+    v = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int r = 0; r < G; ++r) {
+      const uint2 x = *reinterpret_cast<const uint2*>(src + r * D);
+      v.x += u16f<E>(x.x); v.y += u16f<E>(x.x >> 16);
+      v.z += u16f<E>(x.y); v.w += u16f<E>(x.y >> 16);
+    }
+  }
+  if (cos_t != nullptr && col < (Hq + Hkv) * D) {
+    // two interleaved pairs (col, col + 1), (col + 2, col + 3) of one head
+    const int fi = (col % D) >> 1;
+    const long pos = t % S;
+    const float2 c = *reinterpret_cast<const float2*>(cos_t + pos * (D / 2) + fi);
+    const float2 sn = *reinterpret_cast<const float2*>(sin_t + pos * (D / 2) + fi);
+    const float a0 = v.x, b0 = v.y, a1 = v.z, b1 = v.w;
+    // explicit fmas: the in-kernel fold (gqa_fold_rows) rounds identically
+    v.x = fmaf(a0, c.x, b0 * sn.x);
+    v.y = fmaf(-a0, sn.x, b0 * c.x);
+    v.z = fmaf(a1, c.y, b1 * sn.y);
+    v.w = fmaf(-a1, sn.y, b1 * c.y);
+  }
+  uint2 o;
+  o.x = pk2<E>(v.x, v.y);
+  o.y = pk2<E>(v.z, v.w);
+  *reinterpret_cast<uint2*>(dqkv + t * W + col) = o;
+}
+
+// In-kernel GQA fold of the deterministic dK/dV kernel (no finalize pass): every (b, kv head, key
+// tile) has G q-head blocks; each publishes its bf16 partial, fences, and bumps the tile's counter;
+// the block that brings it to G folds the tile's rows (dK / dV over the G partials, RoPE backward
+// of dK and of the group's dQ rows) and re-arms the counter for the next launch.
+struct GqaFold {
+  int* cnt;                // [B * Hkv * key tiles], zero between launches
+  bf16_t* dqkv;            // [T, (Hq + 2 Hkv) D]
+  const float* cos_t;      // RoPE tables or null
+  const float* sin_t;
+  int dbg;                 // timing experiments only (FT_FLASH_FOLD_DBG): 1 no fold work, 2 no release fence
+};
+
+// The fold of `rows` rows from t0 (one key tile of kv head kvh) by NT threads: 16-B units (8
+// columns), U units in flight per thread (loads first, then the sums / rotations / stores: the
+// per-unit load -> add -> store chains otherwise serialise on memory latency). Columns: the G
+// q-heads' dQ (RoPE only, rotated in place), then dK, then dV of the kv head. Sums in head order.
+template <class E, int D, int NT>
+__device__ __forceinline__ void gqa_fold_rows(const bf16_t* __restrict__ dk_part, const bf16_t* __restrict__ dv_part,
+                                              const GqaFold& f, long t0, int rows, int kvh, int G, int Hq, int Hkv,
+                                              int S, int tid) {
+  constexpr int U = 4, CU = D / 8;  // units per thread per pass, units per head row
+  const long W = (long)(Hq + 2 * Hkv) * D;
+  const int uq = f.cos_t != nullptr ? G * CU : 0;
+  const int upr = uq + 2 * CU;
+  const int n = rows * upr;
+  for (int base = 0; base < n; base += NT * U) {
+    uint4 x[U][8];
+    int rr[U], u[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      const int i = base + j * NT + tid;
+      rr[j] = i < n ? i / upr : -1;
+      u[j] = i < n ? i - rr[j] * upr : 0;
+      if (rr[j] < 0) continue;
+      const long t = t0 + rr[j];
+      if (u[j] < uq) {
+        x[j][0] = *reinterpret_cast<const uint4*>(f.dqkv + t * W + (long)kvh * G * D + 8 * u[j]);
+      } else {
+        const bool isk = u[j] < uq + CU;
+        const int c = 8 * (u[j] - uq - (isk ? 0 : CU));
+        const bf16_t* src = (isk ? dk_part : dv_part) + t * Hq * D + (long)kvh * G * D + c;
+#pragma unroll
+        for (int r = 0; r < 8; ++r)
+          if (r < G) x[j][r] = *reinterpret_cast<const uint4*>(src + r * D);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      if (rr[j] < 0) continue;
+      const long t = t0 + rr[j];
+      float v[8];
+      long col;
+      bool rot;
+      auto unpack_add = [&](const uint4& q, bool first) {
+        const unsigned w4[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float lo = u16f<E>(w4[e]), hi = u16f<E>(w4[e] >> 16);
+          v[2 * e] = first ? lo : v[2 * e] + lo;
+          v[2 * e + 1] = first ? hi : v[2 * e + 1] + hi;
+        }
+      };
+      if (u[j] < uq) {
+        unpack_add(x[j][0], true);
+        col = (long)kvh * G * D + 8 * u[j];
+        rot = true;
+      } else {
+        const bool isk = u[j] < uq + CU;
+        const int c = 8 * (u[j] - uq - (isk ? 0 : CU));
+        // 0 + p0 + p1 + ... in head order, as flash_bwd_finalize_kernel
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = 0.f;
+#pragma unroll
+        for (int r = 0; r < 8; ++r)
+          if (r < G) unpack_add(x[j][r], false);
+        col = (isk ? (long)Hq * D : (long)(Hq + Hkv) * D) + (long)kvh * D + c;
+        rot = isk && f.cos_t != nullptr;
+      }
+      if (rot) {
+        const int fi = (int)(col % D) >> 1;
+        const long pos = t % S;
+        const float4 c4 = *reinterpret_cast<const float4*>(f.cos_t + pos * (D / 2) + fi);
+        const float4 s4 = *reinterpret_cast<const float4*>(f.sin_t + pos * (D / 2) + fi);
+        const float cc[4] = {c4.x, c4.y, c4.z, c4.w}, ss[4] = {s4.x, s4.y, s4.z, s4.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float a = v[2 * e], bb = v[2 * e + 1];
+          v[2 * e] = fmaf(a, cc[e], bb * ss[e]);
+          v[2 * e + 1] = fmaf(-a, ss[e], bb * cc[e]);
+        }
+      }
+      uint4 o;
+      o.x = pk2<E>(v[0], v[1]);
+      o.y = pk2<E>(v[2], v[3]);
+      o.z = pk2<E>(v[4], v[5]);
+      o.w = pk2<E>(v[6], v[7]);
+      *reinterpret_cast<uint4*>(f.dqkv + t * W + col) = o;
+    }
+  }
+}
+
 // ================================================================== backward dK/dV, slice pairs (deterministic)
 // flash_bwd_kernel<D, 1> with TWO independent 32-query slices per loop iteration: S / dP
 // of both slices are issued back to back, and in the steady state (both slices fully
@@ -946,7 +1099,8 @@ template <class E, int D, int NW = 4, int SPLIT = 1>
 __global__ __launch_bounds__(64 * NW * SPLIT, SPLIT == 1 ? 4 / NW : 8 / (NW * SPLIT)) void flash_bwd_dkdv2_kernel(
     const bf16_t* __restrict__ dO, const bf16_t* __restrict__ qk, const bf16_t* __restrict__ qkv,
     const float* __restrict__ lse2, const float* __restrict__ delta, bf16_t* __restrict__ dk_part,
-    bf16_t* __restrict__ dv_part, long ldkv, int B, int S, int Hq, int Hkv, float sl2, float scale, long ldqk_) {
+    bf16_t* __restrict__ dv_part, long ldkv, int B, int S, int Hq, int Hkv, float sl2, float scale, long ldqk_,
+    GqaFold fold) {
   constexpr int BK = 32 * NW, BQ = 32, KS = D / 16, NDB = D / 32;
   constexpr int QIMG = BQ * D * 2;          // one Q or dO slice
   constexpr int SLOT = 2 * QIMG + 256;      // Q | dO | lse[32] | delta[32] of one slice
@@ -1159,6 +1313,25 @@ __global__ __launch_bounds__(64 * NW * SPLIT, SPLIT == 1 ? 4 / NW : 8 / (NW * SP
         dv_part[off] = cvt1<E>(dv[db][r]);
       }
     }
+
+  if (fold.cnt != nullptr) {
+    // (SPLIT = 2: half-block 1 has exited; the barriers count the 64 * NW threads left)
+    __shared__ int s_last;
+    const int G = Hq / Hkv;
+    const int ci = (b * Hkv + kvh) * (int)(gridDim.x / per) + kt;
+    // release only (L2 write-back, no invalidate): an acquire here would drop every block's L2
+    // working set; only the folding block needs one
+    if (fold.dbg != 2) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // partial visible device-wide
+    __syncthreads();
+    if (tid == 0) s_last = atomicAdd(fold.cnt + ci, 1) == G - 1;
+    __syncthreads();
+    if (!s_last) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the other G - 1 partials
+    if (tid == 0) fold.cnt[ci] = 0;
+    if (fold.dbg != 1)
+      gqa_fold_rows<E, D, 64 * NW>(dk_part, dv_part, fold, (long)b * S + kb0, min(BK, S - kb0), kvh, G, Hq, Hkv, S,
+                                 tid);
+  }
 }
 
 // ================================================================== backward dQ (deterministic)
@@ -1372,56 +1545,19 @@ __global__ __launch_bounds__(64 * NW * SPLIT, SPLIT == 1 ? 4 / NW : 8 / (NW * SP
 // cos_t != null: the Q and K columns are also rotated back (RoPE backward, reference
 // model.py:100-126 transposed: the interleaved pair (x0, x1) times cis(-theta)), so dqkv is the
 // gradient of the unrotated projection and no separate rope_bwd pass runs; dQ written by the
-// deterministic dQ kernel is rotated in place.
+// deterministic dQ kernel is rotated in place. The deterministic path folds inside the dK/dV kernel
+// (fin_unit from its last GQA block); this pass remains for the other backward variants.
 template <class E>
 __global__ __launch_bounds__(256) void flash_bwd_finalize_kernel(
     const float* __restrict__ dq_acc, const bf16_t* __restrict__ dk_part,
     const bf16_t* __restrict__ dv_part, bf16_t* __restrict__ dqkv, long T, int Hq, int Hkv, int D,
     const float* __restrict__ cos_t, const float* __restrict__ sin_t, int S) {
-  const int G = Hq / Hkv;
   const int W = (Hq + 2 * Hkv) * D;
   const int vpr = W / 4;
   const long total = T * vpr;
   for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
     const long t = i / vpr;
-    const int col = (int)(i - t * vpr) * 4;
-    float4 v;
-    if (col < Hq * D) {
-      if (dq_acc == nullptr) {  // dQ already written by the deterministic dQ kernel
-        if (cos_t == nullptr) continue;
-        const uint2 x = *reinterpret_cast<const uint2*>(dqkv + t * W + col);
-        v = make_float4(u16f<E>(x.x), u16f<E>(x.x >> 16), u16f<E>(x.y), u16f<E>(x.y >> 16));
-      } else {
-        v = *reinterpret_cast<const float4*>(dq_acc + t * Hq * D + col);
-      }
-    } else {
-      const bool isk = col < (Hq + Hkv) * D;
-      const int c2 = col - (isk ? Hq * D : (Hq + Hkv) * D);
-      const int kh = c2 / D, d = c2 % D;
-      const bf16_t* src = (isk ? dk_part : dv_part) + t * Hq * D + (long)kh * G * D + d;
-      v = make_float4(0.f, 0.f, 0.f, 0.f);
-      for (int r = 0; r < G; ++r) {
-        const uint2 x = *reinterpret_cast<const uint2*>(src + r * D);
-        v.x += u16f<E>(x.x); v.y += u16f<E>(x.x >> 16);
-        v.z += u16f<E>(x.y); v.w += u16f<E>(x.y >> 16);
-      }
-    }
-    if (cos_t != nullptr && col < (Hq + Hkv) * D) {
-      // two interleaved pairs (col, col + 1), (col + 2, col + 3) of one head
-      const int fi = (col % D) >> 1;
-      const long pos = t % S;
-      const float2 c = *reinterpret_cast<const float2*>(cos_t + pos * (D / 2) + fi);
-      const float2 sn = *reinterpret_cast<const float2*>(sin_t + pos * (D / 2) + fi);
-      const float a0 = v.x, b0 = v.y, a1 = v.z, b1 = v.w;
-      v.x = a0 * c.x + b0 * sn.x;
-      v.y = -a0 * sn.x + b0 * c.x;
-      v.z = a1 * c.y + b1 * sn.y;
-      v.w = -a1 * sn.y + b1 * c.y;
-    }
-    uint2 o;
-    o.x = pk2<E>(v.x, v.y);
-    o.y = pk2<E>(v.z, v.w);
-    *reinterpret_cast<uint2*>(dqkv + t * W + col) = o;
+    fin_unit<E>(dq_acc, dk_part, dv_part, dqkv, t, (int)(i - t * vpr) * 4, Hq, Hkv, D, cos_t, sin_t, S);
   }
 }
 
@@ -1465,6 +1601,35 @@ bool g_dkdv2_64 = [] {
   const char* e = std::getenv("FT_FLASH_DKDV2");
   return e != nullptr && std::atoi(e) == 2;
 }();
+
+// GQA fold of the deterministic backward in the separate finalize pass (default) or inside the
+// dK/dV kernel by each key tile's last q-head block (FT_FLASH_BWD_FOLD=1 / flash_set_bwd_fold).
+// The in-kernel fold saves the launch but measured slower at the 8B layer (S = 2048, 32/8 heads,
+// RoPE): 296-307 us vs 175-193 us for the whole backward; its device-scope release fences and
+// counters alone cost ~16 us over the finalize variant without any fold work, and the folds run
+// as a 128-block tail behind the heaviest key tiles (profiles/r4_flash_gqa_fold_probe.log).
+bool g_bwd_fold = [] {
+  const char* e = std::getenv("FT_FLASH_BWD_FOLD");
+  return e != nullptr && std::atoi(e) != 0;
+}();
+
+// The fold's per-tile arrival counters: one zeroed int32 buffer per device, grown on demand and
+// kept (each tile's last block re-arms its counter, so the buffer is zero between launches). One
+// backward in flight per device at a time (the training step's single compute stream). Under
+// stream capture a buffer that would have to be (re)allocated is not: the caller falls back to
+// the finalize pass.
+int* fold_counters(const c10::Device& dev, long n) {
+  static std::mutex mu;
+  static std::map<int, at::Tensor> bufs;
+  std::lock_guard<std::mutex> lock(mu);
+  at::Tensor& b = bufs[dev.index()];
+  if (!b.defined() || b.numel() < n) {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(ft_stream(), &st) != hipSuccess || st != hipStreamCaptureStatusNone) return nullptr;
+    b = at::zeros({std::max(n, 4096L)}, at::TensorOptions().device(dev).dtype(at::kInt));
+  }
+  return b.data_ptr<int>();
+}
 
 // Waves (32 query or key rows each) per attention block: 2 when 4-wave blocks would leave
 // most of the 256 CUs idle (fewer than 512 blocks; head_dim 64 — the GPT-2-sized presets:
@@ -1592,6 +1757,15 @@ at::Tensor flash_bwd(const at::Tensor& dout, const at::Tensor& qk, const at::Ten
   const float scale = 1.f / std::sqrt((float)D);
   const long ldqk = qk.size(-1);
   const long rows = (long)T * Hq;
+  // GQA fold inside the deterministic dK/dV kernel (no finalize launch): its tile counters
+  static const int fold_dbg = [] {
+    const char* e = std::getenv("FT_FLASH_FOLD_DBG");
+    return e == nullptr ? 0 : std::atoi(e);
+  }();
+  GqaFold fold{nullptr, mptr<bf16_t>(dqkv), rope ? cptr<float>(*cos_t) : nullptr,
+               rope ? cptr<float>(*sin_t) : nullptr, fold_dbg};
+  if (use_dkdv2 && !direct && g_bwd_fold)
+    fold.cnt = fold_counters(qk.device(), (long)B * Hkv * ((S + 32 * nw_ - 1) / (32 * nw_)));
   const int pre_blocks = (int)((rows * 16 + 255) / 256);
   const int nkt = (S + 127) / 128;
   dim3 grid(nkt * B * Hq), block(256);
@@ -1611,7 +1785,7 @@ at::Tensor flash_bwd(const at::Tensor& dout, const at::Tensor& qk, const at::Ten
   hipLaunchKernelGGL((flash_bwd_dkdv2_kernel<E, DD, NW_, SP_>), grid2, dim3(64 * NW_ * SP_), 0, ft_stream(), \
                      cptr<bf16_t>(dout), cptr<bf16_t>(qk), cptr<bf16_t>(qkv), cptr<float>(lse),           \
                      cptr<float>(delta), dkp, dvp, ldkv, B, (int)S,                                       \
-                     (int)Hq, (int)Hkv, sl2, scale, ldqk)
+                     (int)Hq, (int)Hkv, sl2, scale, ldqk, fold)
   // dQ key split by default (FT_FLASH_DQ_SPLIT=0 turns it off): S = 2048, 12 heads of 64:
   // 94 -> 83 us for the whole backward; 8B layer 173 -> 167 us; S = 16384 1006 -> 972 us
   // (profiles/r2_flash_key_split.log)
@@ -1663,6 +1837,7 @@ at::Tensor flash_bwd(const at::Tensor& dout, const at::Tensor& qk, const at::Ten
     if (rope) rope_bwd_(dqkv, *cos_t, *sin_t, S, Hq, Hkv, D);
     return dqkv;
   }
+  if (fold.cnt != nullptr) return dqkv;  // folded by the dK/dV kernel's last block per tile
   const long vec = (long)T * ((Hq + 2 * Hkv) * D / 4);
   const int fin_blocks = (int)std::max(1L, std::min((vec + 255) / 256, 4096L));
   FT_DISPATCH_E16(qk.scalar_type(),
@@ -1682,6 +1857,7 @@ void flash_set_fwd_split(int64_t v) { g_fwd_split = (int)v; }
 void flash_set_dq_split(int64_t v) { g_dq_split = (int)v; }
 void flash_set_fwd_pipe(int64_t v) { g_fwd_pipe = (int)v; }
 void flash_set_kv_split(int64_t v) { g_kv_split = (int)v; }
+void flash_set_bwd_fold(bool on) { g_bwd_fold = on; }
 
 TORCH_LIBRARY_FRAGMENT(ftamd, m) {
   m.def("flash_set_dkdv2(bool on) -> ()", &flash_set_dkdv2);
@@ -1689,6 +1865,7 @@ TORCH_LIBRARY_FRAGMENT(ftamd, m) {
   m.def("flash_set_dq_split(int v) -> ()", &flash_set_dq_split);
   m.def("flash_set_fwd_pipe(int v) -> ()", &flash_set_fwd_pipe);
   m.def("flash_set_kv_split(int v) -> ()", &flash_set_kv_split);
+  m.def("flash_set_bwd_fold(bool on) -> ()", &flash_set_bwd_fold);
   m.def("flash_fwd(Tensor qk, Tensor qkv, int S, int Hq, int Hkv, int D) -> (Tensor, Tensor)",
         &flash_fwd);
   m.def(

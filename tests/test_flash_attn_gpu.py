@@ -247,3 +247,32 @@ def test_flash_bwd_with_rope_backward(B, S, Hq, Hkv, D, mode):
         assert rel(got[:, lo:hi], ref[:, lo:hi]) < 4e-3, (lo, hi)
     if mode == 1:
         assert torch.equal(got, K.flash_bwd(do, qk, qkv, o, lse, S, Hq, Hkv, D, mode, cos, sin))
+
+
+@pytest.mark.parametrize("B,S,Hq,Hkv,D,rope", [(1, 2048, 32, 8, 128, True), (2, 320, 8, 2, 128, False),
+                                               (1, 1000, 4, 1, 128, True), (2, 512, 8, 2, 64, True),
+                                               (1, 100, 6, 2, 64, False)])
+def test_flash_bwd_in_kernel_gqa_fold(B, S, Hq, Hkv, D, rope):
+    """Deterministic backward, opt-in variant (FT_FLASH_BWD_FOLD=1): the GQA fold (+ RoPE backward)
+    done by the last q-head block of each key tile inside the dK/dV kernel == the finalize pass, bit
+    for bit (same head order), and stays so over repeated launches (the counters re-arm)."""
+    from fault_tolerant_llm_training_amd._native import kernels
+    from fault_tolerant_llm_training_amd.models.llama import rope_tables
+
+    K = kernels()
+    torch.manual_seed(6)
+    T = B * S
+    qkv = torch.randn(T, (Hq + 2 * Hkv) * D, device="cuda").bfloat16()
+    qk = torch.randn(T, (Hq + Hkv) * D, device="cuda").bfloat16()
+    do = torch.randn(T, Hq * D, device="cuda").bfloat16()
+    cs = tuple(t.cuda() for t in rope_tables(D, S, 500000.0)) if rope else (None, None)
+    o, lse = K.flash_fwd(qk, qkv, S, Hq, Hkv, D)
+    try:
+        K.flash_set_bwd_fold(False)
+        ref = K.flash_bwd(do, qk, qkv, o, lse, S, Hq, Hkv, D, 1, *cs)
+        K.flash_set_bwd_fold(True)
+        outs = [K.flash_bwd(do, qk, qkv, o, lse, S, Hq, Hkv, D, 1, *cs) for _ in range(3)]
+    finally:
+        K.flash_set_bwd_fold(False)
+    for g in outs:
+        assert torch.equal(g, ref)
