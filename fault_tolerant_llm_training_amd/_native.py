@@ -36,6 +36,16 @@ def _missing(path: Path) -> NativeExtensionMissing:
     )
 
 
+# dtypes the gfx950 kernels cover; a CUDA tensor of another dtype (fp64 models, --model-dtype fp64)
+# takes the composed-PyTorch path that CPU tensors take
+NATIVE_DTYPES = (torch.bfloat16, torch.float16, torch.float32)
+
+
+def native(t: torch.Tensor) -> bool:
+    """True when ``t`` is handled by the HIP kernels (a GPU tensor of a kernel dtype)."""
+    return t.is_cuda and t.dtype in NATIVE_DTYPES
+
+
 def kernels():
     """Return ``torch.ops.ftamd`` after loading ``_kernels.so`` (raises if absent)."""
     global _kernels_loaded

@@ -27,7 +27,7 @@ from typing import Optional
 import torch
 import torch.nn.functional as F
 
-from .._native import kernels
+from .._native import kernels, native
 from .grad_sink import GradSink
 
 IGNORE_INDEX = -100
@@ -430,7 +430,7 @@ class EmbeddingFn(torch.autograd.Function):
         ctx.vocab = weight.shape[0]
         ctx.save_for_backward(tokens)
         ctx.wshape = weight.shape
-        if weight.is_cuda:
+        if native(weight):
             return kernels().embedding_fwd(tokens.contiguous(), weight)
         return F.embedding(tokens, weight)
 
@@ -449,7 +449,7 @@ class EmbeddingFn(torch.autograd.Function):
                 sink.stash = []
             # DP sparse exchange: every rank's (token, dY) rows, scatter-added locally
             tokens, dy = sink.gather(tokens, dy)
-        if dy.is_cuda:
+        if native(dy):
             if sink is None:
                 dw = torch.zeros(ctx.wshape, dtype=dy.dtype, device=dy.device)
                 kernels().embedding_bwd_(dy, tokens.contiguous(), dw, False)
@@ -481,7 +481,7 @@ class NormFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, sink, eps, layernorm):
         ctx.sink, ctx.eps, ctx.ln = sink, eps, layernorm
-        if x.is_cuda:
+        if native(x):
             xc = x.contiguous()
             y, rstd, mean = kernels().norm_fwd(xc, weight, eps, layernorm)
             ctx.save_for_backward(xc, weight, rstd, mean)
@@ -492,7 +492,7 @@ class NormFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         sink = ctx.sink
-        if dy.is_cuda:
+        if native(dy):
             x, w, rstd, mean = ctx.saved_tensors
             if sink is not None:
                 return norm_bwd_into_sink(dy.contiguous(), x, w, rstd, mean, sink), None, None, None, None
@@ -522,7 +522,7 @@ class AddNormFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, d, weight, sink, eps, layernorm):
         ctx.sink, ctx.eps, ctx.ln = sink, eps, layernorm
-        if x.is_cuda:
+        if native(x):
             y, rstd, mean, h = kernels().add_norm_fwd(x.contiguous(), d.contiguous(), weight, eps, layernorm)
             ctx.save_for_backward(h, weight, rstd, mean)
             return h, y
@@ -533,7 +533,7 @@ class AddNormFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dh, dy):
         sink = ctx.sink
-        if dy.is_cuda:
+        if native(dy):
             h, w, rstd, mean = ctx.saved_tensors
             dres = dh.contiguous() if dh is not None else None
             if sink is not None:
@@ -645,7 +645,7 @@ class RopeAttentionFn(torch.autograd.Function):
         ctx.cfg = (seq_len, hq, hkv, d)
         ctx.rotated = rotated
         hit = keep is not None and keep.gen == gen and keep.o is not None
-        if qkv.is_cuda:
+        if native(qkv):
             from .attention import flash_attn_fwd
 
             qkv = qkv.contiguous()
@@ -672,7 +672,7 @@ class RopeAttentionFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, do):
         seq_len, hq, hkv, d = ctx.cfg
-        if do.is_cuda:
+        if native(do):
             from .attention import flash_attn_bwd
 
             qkv, qk, o, lse, cos, sin = ctx.saved_tensors
@@ -762,14 +762,14 @@ class SwiGLUFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, gu):
         ctx.save_for_backward(gu)
-        if gu.is_cuda:
+        if native(gu):
             return kernels().swiglu_fwd(gu.contiguous())
         return swiglu_reference(gu)
 
     @staticmethod
     def backward(ctx, da):
         (gu,) = ctx.saved_tensors
-        if da.is_cuda:
+        if native(da):
             return kernels().swiglu_bwd(da.contiguous(), gu.contiguous())
         with torch.enable_grad():
             x = gu.detach().requires_grad_(True)
@@ -960,7 +960,7 @@ class FusedFFNFn(torch.autograd.Function):
 
 def feed_forward(x, w13, w2, sink13=None, sink2=None):
     """SwiGLU FFN on the fused [w1; w3] weight; fused node on the GPU, composed ops on CPU."""
-    if x.is_cuda and _FUSED_FFN:
+    if native(x) and _FUSED_FFN:
         T, D = x.numel() // x.shape[-1], x.shape[-1]
         F = w13.shape[0] // 2
         if _ffn_w4t_ok(x.reshape(T, D), w13, w2):
@@ -1080,7 +1080,7 @@ class LMHeadCrossEntropyFn(torch.autograd.Function):
         lab = labels.reshape(-1)
         ctx.sink = sink
         ctx.hshape = h.shape
-        if not h.is_cuda:
+        if not native(h):
             logits = torch.mm(h2, weight.t())
             loss = F.cross_entropy(logits.float(), lab, reduction="sum", ignore_index=IGNORE_INDEX) * inv_count
             ctx.save_for_backward(h2, weight, lab, inv_count)
@@ -1123,7 +1123,7 @@ class LMHeadCrossEntropyFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         sink = ctx.sink
-        if not g.is_cuda:
+        if not native(g):
             h2, w, lab, inv_count = ctx.saved_tensors
             with torch.enable_grad():
                 hr = h2.detach().requires_grad_(True)

@@ -41,7 +41,7 @@ from typing import List, Optional, Tuple
 import torch
 import torch.distributed as dist
 
-from .._native import kernels
+from .._native import kernels, native
 from ..models.flat import FlatParamSpace
 
 
@@ -167,7 +167,7 @@ class FlatAdamW(torch.optim.Optimizer):
         self.hyper.copy_(h, non_blocking=True)
 
     def _update(self, p, g, m, v, lr, b1, b2, eps, wd, max_blocks: int = 0):
-        if p.is_cuda:
+        if native(p):
             kernels().adamw_(p, g, m, v, self.stats, lr, b1, b2, eps, wd, self.step_count, max_blocks,
                              self.hyper if self.graph_mode else None)
         else:
@@ -186,6 +186,7 @@ class FlatAdamW(torch.optim.Optimizer):
                 from ..ops.functional import join_dw_stream
 
                 join_dw_stream()
+            if native(f.grads):
                 kernels().grad_norm_(f.grads, self.stats, self.max_grad_norm)
             else:
                 _norm_reference(f.grads.float().pow(2).sum().reshape(1), self.stats, self.max_grad_norm)

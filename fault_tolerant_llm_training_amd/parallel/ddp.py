@@ -57,7 +57,7 @@ from typing import List, Optional
 import torch
 import torch.distributed as dist
 
-from .._native import kernels
+from .._native import kernels, native
 from ..models.flat import FlatParamSpace
 from ..ops.grad_sink import GradSink
 
@@ -207,7 +207,7 @@ class GradReducer:
         self.overlap = self.cuda if overlap is None else (overlap and self.cuda)
         # partial sums of squares: a fixed slice per bucket (or per sink, FUSED_SUMSQ) -> the
         # total is a fixed-order sum, deterministic
-        self.fused_sumsq = FUSED_SUMSQ and mode == "local" and self.cuda and self.overlap
+        self.fused_sumsq = FUSED_SUMSQ and mode == "local" and native(flat.grads) and self.overlap
         self._sq_sinks: List[GradSink] = []
         self._bucket_sq_sinks: List[List[GradSink]] = [[] for _ in self.buckets]
         p = 0
@@ -363,7 +363,7 @@ class GradReducer:
                 sink.sq_done = False
             return
         part = self.partials[b.part_lo : b.part_hi]
-        if g.is_cuda:
+        if native(g):
             kernels().sumsq_into_(g, part)
         else:
             part.zero_()

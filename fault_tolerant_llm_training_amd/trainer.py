@@ -214,8 +214,11 @@ def train(args) -> int:
     monitor = SignalMonitor().install()
     device = info.device
     model_dtype = PRECISION_STR_TO_DTYPE[args.model_dtype]
-    if device.type == "cuda" and model_dtype not in (torch.bfloat16, torch.float16, torch.float32):
-        raise ValueError("the gfx950 kernels cover --model-dtype bf16, fp16 and fp32 (fp64 on --device cpu only)")
+    if device.type == "cuda" and model_dtype == torch.float64:
+        # the reference builds the model in fp64 on the GPU too (utils.py:14-19, train.py:54-59); the
+        # gfx950 kernels cover bf16 / fp16 / fp32, so fp64 tensors take the composed-PyTorch path
+        # (rocBLAS dgemm, reference attention): correct, not fast
+        logger.info("--model-dtype fp64 on the GPU: composed PyTorch ops (the HIP kernels cover bf16/fp16/fp32)")
     torch.manual_seed(args.seed)
     from .ops.attention import set_deterministic
 

@@ -226,14 +226,36 @@ def test_model_gpu_vs_cpu(dt, preset, V, S):
     assert rel(mg.flat.grads.cpu(), mc.flat.grads) < (2e-2 if dt == torch.float16 else 1e-4)
 
 
+def test_model_gpu_fp64_vs_cpu():
+    """--model-dtype fp64 on the GPU (no HIP kernel covers fp64: composed PyTorch ops on the device)
+    == the fp64 CPU model with the same weights, loss and gradients to fp64 rounding."""
+    from fault_tolerant_llm_training_amd.models.llama import build_model, model_args_for
+
+    a = model_args_for("tiny", vocab_size=512, seq_len=128)
+    mg = build_model(a, "cuda", torch.float64, seed=7)
+    mc = build_model(a, "cpu", torch.float64, seed=7)
+    mc.load_state_dict({k: v.cpu() for k, v in mg.state_dict().items()})
+    torch.manual_seed(3)
+    tok = torch.randint(0, 512, (2, 128))
+    lab = torch.randint(0, 512, (2, 128))
+    lg = mg(tok.cuda(), lab.cuda())
+    lc = mc(tok, lab)
+    lg.backward()
+    lc.backward()
+    assert mg.flat.grads.dtype == torch.float64 and mg.flat.grads.is_cuda
+    assert abs(lg.item() - lc.item()) < 1e-10 * abs(lc.item())
+    assert rel(mg.flat.grads.cpu(), mc.flat.grads) < 1e-10
+
+
 GPU = ["--device", "cuda", "--synthetic-data", "--vocab-size", "1024", "--sequence-length", "256",
        "--batch-size", "2", "--learning-rate", "1e-3", "--lr-warmup-steps", "3", "--logging-frequency", "5"]
 
 
-@pytest.mark.parametrize("dt", ["fp16", "fp32"])
+@pytest.mark.parametrize("dt", ["fp16", "fp32", "fp64"])
 def test_train_error_save_resume_bit_exact(tmp_path, dt):
-    """train.py --model-dtype fp16 / fp32 on the GPU: an injected error saves, the resumed job
-    ends bit-identical to an uninterrupted one, and the losses stay finite and bounded."""
+    """train.py --model-dtype fp16 / fp32 / fp64 on the GPU (fp64: the composed-PyTorch path, as the
+    reference allows, utils.py:14-19): an injected error saves, the resumed job ends bit-identical
+    to an uninterrupted one, and the losses stay finite and bounded."""
     from helpers import run_train, write_fake_sbatch
 
     d = str(tmp_path)
@@ -253,7 +275,7 @@ def test_train_error_save_resume_bit_exact(tmp_path, dt):
     ld = lambda j: torch.load(os.path.join(d, "ck", f"checkpoint_{j}.ckpt"), map_location="cpu",
                               weights_only=True)
     a, c = ld(800), ld(802)
-    want = {"fp16": torch.float16, "fp32": torch.float32}[dt]
+    want = {"fp16": torch.float16, "fp32": torch.float32, "fp64": torch.float64}[dt]
     for k in a["model"]:
         assert a["model"][k].dtype == want
         assert torch.equal(a["model"][k], c["model"][k]), k
