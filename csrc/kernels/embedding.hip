@@ -18,6 +18,8 @@
 // goes to bin start + earlier rounds + earlier waves + its rank — i.e. stably.
 #include "torch_utils.h"
 
+#include <algorithm>
+
 namespace {
 
 // row copy in 16-B vectors (any element size; rows are whole vectors)
@@ -134,6 +136,49 @@ __global__ __launch_bounds__(256) void emb_bwd_kernel(const int* __restrict__ so
   }
 }
 
+// emb_bwd_kernel for a fresh (zeroed) gradient, plus the gradient-norm partials of what it stores:
+// every row it does not write is zero, so the sum of squares of the whole [V, D] gradient is the
+// sum over the written rows — no pass over the 1 GB buffer (the 8B vocabulary). Block b takes
+// segment waves b*4 .. in a grid-stride loop, each lane its columns in a fixed order, and writes
+// part[b]; the remaining partial slots are zeroed. Fixed order throughout: deterministic.
+template <class E>
+__global__ __launch_bounds__(256) void emb_bwd_sq_kernel(const int* __restrict__ sorted_tok,
+                                                         const int* __restrict__ perm,
+                                                         const typename E::T* __restrict__ dy,
+                                                         typename E::T* __restrict__ dw, int T, int D,
+                                                         float* __restrict__ part, int nparts) {
+  __shared__ float red[4];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  float sq = 0.f;
+  for (int wave = blockIdx.x * 4 + wid; wave < T; wave += gridDim.x * 4) {
+    const int t = sorted_tok[wave];
+    if (wave > 0 && sorted_tok[wave - 1] == t) continue;  // not the segment head
+    int end = wave + 1;
+    while (end < T && sorted_tok[end] == t) ++end;
+    typename E::T* dst = dw + t * (long)D;
+    for (int c = lane * 8; c < D; c += 64 * 8) {
+      float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      for (int k = wave; k < end; ++k) {
+        float x[8];
+        ld8<E>(dy + perm[k] * (long)D + c, x);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += x[j];
+      }
+      const P8<E> r = pk8<E>(acc);
+      *reinterpret_cast<uint4*>(dst + c) = r.v[0];
+      if constexpr (!E::is16) *reinterpret_cast<uint4*>(dst + c + 4) = r.v[1];
+      float st[8];
+      unp8<E>(r, st);  // the stored (rounded) values
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sq = fmaf(st[j], st[j], sq);
+    }
+  }
+  const float tot = block_sum<256>(sq, red);
+  if (threadIdx.x == 0) part[blockIdx.x] = tot;
+  for (long i = blockIdx.x + (long)gridDim.x * (1 + threadIdx.x); i < nparts; i += (long)gridDim.x * 256)
+    part[i] = 0.f;
+}
+
 }  // namespace
 
 at::Tensor embedding_fwd(const at::Tensor& tokens, const at::Tensor& weight) {
@@ -156,9 +201,10 @@ at::Tensor embedding_fwd(const at::Tensor& tokens, const at::Tensor& weight) {
   return out;
 }
 
-// Writes (or accumulates) the dense gradient into dw [V, D].
+// Writes (or accumulates) the dense gradient into dw [V, D]. part (fp32, not accumulating): also
+// the gradient-norm partial sums of the written gradient (see emb_bwd_sq_kernel).
 void embedding_bwd_(const at::Tensor& dy, const at::Tensor& tokens, const at::Tensor& dw,
-                    bool accumulate) {
+                    bool accumulate, const std::optional<at::Tensor>& part) {
   FT_CHECK_CUDA(dy);
   FT_CHECK_MODEL_DTYPE(dy);
   TORCH_CHECK(dy.scalar_type() == dw.scalar_type(), "embedding_bwd: dtype mismatch");
@@ -185,15 +231,31 @@ void embedding_bwd_(const at::Tensor& dy, const at::Tensor& tokens, const at::Te
     FT_LAUNCH_CHECK();
     const long fin = (long)((passes - 1) & 1) * T;
     const int blocks = (T * 64 + 255) / 256;
-    FT_DISPATCH_E(dy.scalar_type(),
-                  hipLaunchKernelGGL(emb_bwd_kernel<E>, dim3(blocks), dim3(256), 0, ft_stream(), keys + fin,
-                                     vals + fin, cptr<typename E::T>(dy), mptr<typename E::T>(dw), T, D, accumulate));
+    const bool sq = part.has_value() && part->defined();
+    if (sq) {
+      TORCH_CHECK(!accumulate, "embedding_bwd: norm partials need a fresh gradient");
+      FT_CHECK_F32((*part));
+      FT_CHECK_CONTIG((*part));
+      const int np = (int)part->numel();
+      const int g = std::max(1, std::min({blocks, 256, np}));
+      FT_DISPATCH_E(dy.scalar_type(),
+                    hipLaunchKernelGGL(emb_bwd_sq_kernel<E>, dim3(g), dim3(256), 0, ft_stream(), keys + fin,
+                                       vals + fin, cptr<typename E::T>(dy), mptr<typename E::T>(dw), T, D,
+                                       mptr<float>(*part), np));
+    } else {
+      FT_DISPATCH_E(dy.scalar_type(),
+                    hipLaunchKernelGGL(emb_bwd_kernel<E>, dim3(blocks), dim3(256), 0, ft_stream(), keys + fin,
+                                       vals + fin, cptr<typename E::T>(dy), mptr<typename E::T>(dw), T, D,
+                                       accumulate));
+    }
+  } else if (part.has_value() && part->defined()) {
+    part->zero_();
   }
   FT_LAUNCH_CHECK();
 }
 
 TORCH_LIBRARY_FRAGMENT(ftamd, m) {
   m.def("embedding_fwd(Tensor tokens, Tensor weight) -> Tensor", &embedding_fwd);
-  m.def("embedding_bwd_(Tensor dy, Tensor tokens, Tensor(a!) dw, bool accumulate) -> ()",
+  m.def("embedding_bwd_(Tensor dy, Tensor tokens, Tensor(a!) dw, bool accumulate, Tensor(b!)? part=None) -> ()",
         &embedding_bwd_);
 }

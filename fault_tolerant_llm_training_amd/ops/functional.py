@@ -454,7 +454,12 @@ class EmbeddingFn(torch.autograd.Function):
                 dw = torch.zeros(ctx.wshape, dtype=dy.dtype, device=dy.device)
                 kernels().embedding_bwd_(dy, tokens.contiguous(), dw, False)
                 return None, dw, None
-            kernels().embedding_bwd_(dy, tokens.contiguous(), sink.buf, sink.accumulate)
+            # a fresh gradient: the kernel also writes the norm partials of the rows it stores (every
+            # other row is zero), so the reducer's sum-of-squares pass over the [V, D] buffer is skipped
+            part = sink.part if (sink.part is not None and not sink.accumulate) else None
+            kernels().embedding_bwd_(dy, tokens.contiguous(), sink.buf, sink.accumulate, part)
+            if part is not None:
+                sink.sq_done = True
             sink.ready()
             return None, None, None
         dw = torch.zeros(ctx.wshape, dtype=torch.float32, device=dy.device)

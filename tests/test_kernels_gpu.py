@@ -446,3 +446,26 @@ def test_exact_math_switch(K):
         ulp = b.float().abs() * 2.0 ** -7 + 1e-30
         assert (diff <= ulp).all()
         assert (diff > 0).float().mean().item() < 0.02
+
+
+@pytest.mark.parametrize("V,T,ntok,nparts", [(131072, 2048, 131072, 16384), (1000, 300, 40, 7), (5000, 4096, 3000, 300)])
+def test_embedding_bwd_norm_partials(K, V, T, ntok, nparts):
+    """embedding_bwd_ with partials (fresh gradient): the same gradient as without, every partial
+    slot written (stale values cleared), their sum = the sum of squares of the stored gradient,
+    bit-reproducible."""
+    D = 256
+    torch.manual_seed(V + T)
+    tok = torch.randint(0, ntok, (T,), device="cuda")
+    dy = torch.randn(T, D, device="cuda").bfloat16()
+    ref = torch.zeros(V, D, device="cuda").bfloat16()
+    K.embedding_bwd_(dy, tok, ref, False)
+    dw = torch.full((V, D), 3.0, device="cuda").bfloat16()
+    part = torch.full((nparts,), -5.0, device="cuda")
+    K.embedding_bwd_(dy, tok, dw, False, part)
+    assert torch.equal(dw, ref)
+    want = ref.double().pow(2).sum().item()
+    assert abs(part.double().sum().item() - want) <= 1e-5 * want
+    assert torch.all(part >= 0)
+    part2 = torch.zeros(nparts, device="cuda")
+    K.embedding_bwd_(dy, tok, dw, False, part2)
+    assert torch.equal(part2, part)
