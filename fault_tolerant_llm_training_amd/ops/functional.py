@@ -1085,7 +1085,8 @@ class LMHeadCrossEntropyFn(torch.autograd.Function):
         lab = labels.reshape(-1)
         ctx.sink = sink
         ctx.hshape = h.shape
-        if not native(h):
+        ctx.native = native(h)  # (backward's g is the fp32 loss gradient whatever the model dtype)
+        if not ctx.native:
             logits = torch.mm(h2, weight.t())
             loss = F.cross_entropy(logits.float(), lab, reduction="sum", ignore_index=IGNORE_INDEX) * inv_count
             ctx.save_for_backward(h2, weight, lab, inv_count)
@@ -1128,7 +1129,7 @@ class LMHeadCrossEntropyFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         sink = ctx.sink
-        if not native(g):
+        if not ctx.native:
             h2, w, lab, inv_count = ctx.saved_tensors
             with torch.enable_grad():
                 hr = h2.detach().requires_grad_(True)
