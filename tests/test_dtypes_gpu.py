@@ -228,7 +228,8 @@ def test_model_gpu_vs_cpu(dt, preset, V, S):
 
 def test_model_gpu_fp64_vs_cpu():
     """--model-dtype fp64 on the GPU (no HIP kernel covers fp64: composed PyTorch ops on the device)
-    == the fp64 CPU model with the same weights, loss and gradients to fp64 rounding."""
+    == the fp64 CPU model with the same weights (the cross-entropy runs in fp32 on both, as in the
+    reference's logits.float(): agreement to fp32 rounding)."""
     from fault_tolerant_llm_training_amd.models.llama import build_model, model_args_for
 
     a = model_args_for("tiny", vocab_size=512, seq_len=128)
@@ -243,8 +244,8 @@ def test_model_gpu_fp64_vs_cpu():
     lg.backward()
     lc.backward()
     assert mg.flat.grads.dtype == torch.float64 and mg.flat.grads.is_cuda
-    assert abs(lg.item() - lc.item()) < 1e-10 * abs(lc.item())
-    assert rel(mg.flat.grads.cpu(), mc.flat.grads) < 1e-10
+    assert abs(lg.item() - lc.item()) < 1e-6 * abs(lc.item())
+    assert rel(mg.flat.grads.cpu(), mc.flat.grads) < 1e-5
 
 
 GPU = ["--device", "cuda", "--synthetic-data", "--vocab-size", "1024", "--sequence-length", "256",
