@@ -463,7 +463,11 @@ class EmbeddingFn(torch.autograd.Function):
             sink.ready()
             return None, None, None
         dw = torch.zeros(ctx.wshape, dtype=torch.float32, device=dy.device)
-        dw.index_add_(0, tokens.reshape(-1), dy.reshape(-1, ctx.wshape[1]).float())
+        if dy.is_cuda:  # (fp64 models on the GPU) index_add_ is atomic there; the sorted
+            # accumulate of index_put_ is deterministic (bit-exact resume)
+            dw.index_put_((tokens.reshape(-1),), dy.reshape(-1, ctx.wshape[1]).float(), accumulate=True)
+        else:
+            dw.index_add_(0, tokens.reshape(-1), dy.reshape(-1, ctx.wshape[1]).float())
         return None, _write_weight_grad(sink, dw.to(dy.dtype)), None
 
 
