@@ -9,6 +9,7 @@ zip writer) and the pinned-ring restore. Checked here:
 * SIGUSR1 saves and resubmits through ``sbatch`` with the job id (reference utils.py:81-85).
 """
 import os
+import shutil
 import signal
 
 import pytest
@@ -146,13 +147,19 @@ def test_gpu_llama8b_iterable_error_resume_bit_exact(tmp_path):
         assert m, out[-3000:]
         return int(m.group(1)), m.group(2).strip()
 
-    rc, out = run_train(d, "790", base, timeout=600)
-    assert rc == 0 and "Training completed" in out, out[-3000:]
-    ref = digest(out)
-    assert ref[0] == 12
-    rc, out = run_train(d, "791", base + ["--raise-error", "--error-step", "5"], timeout=600)
-    assert rc == 0 and "Checkpoint saved at step 5" in out, out[-3000:]
-    rc, out = run_train(d, "792", base + ["--checkpoint-id", "791"], timeout=600)
-    assert rc == 0 and "Resuming training from training_step 5" in out, out[-3000:]
-    assert "Data loader position restored" in out
-    assert digest(out) == ref
+    try:
+        rc, out = run_train(d, "790", base, timeout=600)
+        assert rc == 0 and "Training completed" in out, out[-3000:]
+        ref = digest(out)
+        assert ref[0] == 12
+        rc, out = run_train(d, "791", base + ["--raise-error", "--error-step", "5"], timeout=600)
+        assert rc == 0 and "Checkpoint saved at step 5" in out, out[-3000:]
+        saved = re.search(r"State digest at step 5 \(saved\): (.*)", out)
+        rc, out = run_train(d, "792", base + ["--checkpoint-id", "791"], timeout=600)
+        assert rc == 0 and "Resuming training from training_step 5" in out, out[-3000:]
+        assert "Data loader position restored" in out
+        resumed = re.search(r"State digest at step 5 \(resumed\): (.*)", out)
+        assert saved and resumed and saved.group(1).strip() == resumed.group(1).strip()
+        assert digest(out) == ref
+    finally:  # the 48 GB checkpoint: pytest keeps tmp dirs, and later jobs on the box need the disk
+        shutil.rmtree(os.path.join(d, "ck"), ignore_errors=True)
