@@ -307,6 +307,9 @@ def train(args) -> int:
             g["lr"] = lr
         logger.info("LR Scheduler loaded from checkpoint")
         restore_rng(checkpoint.get("rng"), device)
+    # loader position before each step (what a checkpoint taken at that step boundary records)
+    loader_at: Dict[int, Any] = {}
+
     def log_digest(step: int, when: str = "") -> None:
         """--state-digest: an order-independent digest of params / moments + the loader position,
         comparable across a save (exit handler) and the resume from it, or across two runs."""
@@ -315,9 +318,12 @@ def train(args) -> int:
         from .utils.digest import state_digest
 
         dg = state_digest(model.flat.params, optimizer.exp_avg, optimizer.exp_avg_sq)
+        # the loader position a checkpoint at this step boundary records (the live loader may
+        # already have fetched the next batch when a signal stops the run)
+        pos = loader_at.get(step, loader.state_dict())
         logger.info(f"[rank {info.rank}] State digest at step {step}{when}: params={dg['params']} "
                     f"exp_avg={dg['exp_avg']} exp_avg_sq={dg['exp_avg_sq']} "
-                    f"optimizer_step={optimizer.step_count} data_loader={json.dumps(loader.state_dict(), sort_keys=True)}")
+                    f"optimizer_step={optimizer.step_count} data_loader={json.dumps(pos, sort_keys=True)}")
 
     if checkpoint is not None:
         training_step = int(checkpoint["training_step"])
@@ -377,8 +383,6 @@ def train(args) -> int:
         # SIGUSR1 one, racing the Slurm deadline) then only copies and writes
         ckpt_engine().preallocate_async()
 
-    # loader position before each step (what a checkpoint taken at that step boundary records)
-    loader_at: Dict[int, Any] = {}
 
     def save_checkpoint(blocking: bool, step_now: int):
         """Collective save of the state at step boundary ``step_now`` (every rank calls it)."""

@@ -206,6 +206,33 @@ def test_sigusr1_preempt_resume_loses_zero_steps(tmp_path):
     _assert_same_state(_final_state(_ckpt(d, "50")), _final_state(_ckpt(d, "70")))
 
 
+def test_sigusr1_state_digest_saved_equals_resumed_iterable(tmp_path):
+    """SIGUSR1 mid-run on the iterable dataset (the loader has usually fetched the next batch when
+    the signal is acted on): the digest logged at the exit-handler save, loader position included,
+    equals the one logged after the next job resumed from that checkpoint."""
+    d = str(tmp_path)
+    write_fake_sbatch(d)
+    pq = os.path.join(d, "data.parquet")
+    make_parquet(pq, n_docs=60)
+    base = (TINY + ["--dataset", pq, "--tokenizer-name-or-path", "byte", "--iterable-dataset", "--state-digest"]
+            + _common(d) + ["--training-steps", "100000", "--lr-warmup-steps", "4"])
+    p = start_train(d, "61", base)
+    try:
+        assert wait_for_log(p._log_path, "Training step: 10 |")
+        os.kill(p.pid, signal.SIGUSR1)
+        assert p.wait(timeout=120) == 0
+    finally:
+        kill_group(p)
+    out = open(p._log_path).read()
+    saved = re.search(r"State digest at step (\d+) \(saved\): (.*)", out)
+    assert saved and "Job timed out" in out, out[-3000:]
+    rc, out = run_train(d, "62", base[:-4] + ["--training-steps", str(int(saved.group(1)) + 1), "--lr-warmup-steps",
+                                              "4", "--checkpoint-id", "61"])
+    assert rc == 0, out[-3000:]
+    resumed = re.search(r"State digest at step (\d+) \(resumed\): (.*)", out)
+    assert resumed and resumed.groups() == saved.groups(), (saved.groups(), resumed and resumed.groups())
+
+
 def test_periodic_async_checkpoint(tmp_path):
     d = str(tmp_path)
     rc, out = run_train(d, "80", SYN + _common(d) + ["--training-steps", "9", "--save-every", "4"])
