@@ -544,7 +544,40 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(W4Args p) {
   __builtin_amdgcn_wave_barrier();
   const int cc = lane & 15;
   float sq = 0.f;  // sum of squares of the stored values (p.part)
-  if (cc < 2 * NJ) {
+  if constexpr (EPI == W4_SWIGLU_BWD) {
+    // dgu from da (LDS) and the saved gu (global): the gu rows of 16 tile rows are loaded before
+    // any is used (the fragment registers are free now), so the epilogue waits on HBM latency twice
+    // per tile instead of once per 4 rows
+    if (cc < 2 * NJ) {
+      const int gn = n0 + wn * NW + cc * 8;
+#pragma unroll
+      for (int hb = 0; hb < 2; ++hb) {
+        uint4 g16[16], u16[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const long gm = m0 + wm * 128 + (hb * 16 + q) * 4 + (lane >> 4);
+          g16[q] = *reinterpret_cast<const uint4*>(p.r + gm * p.ldr + gn);
+          u16[q] = *reinterpret_cast<const uint4*>(p.r + gm * p.ldr + p.ffn + gn);
+        }
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const int row = (hb * 16 + q) * 4 + (lane >> 4);
+          const long gm = m0 + wm * 128 + row;
+          const uint4 v = *reinterpret_cast<const uint4*>(wl + row * 256 + ((cc ^ (row & 15)) << 4));
+          // v = da (bf16, as the unfused path's GEMM output) for features gn .. gn + 7 of token gm:
+          // dg, du from the saved g = gu[gm, gn], u = gu[gm, F + gn] (swiglu_grad, common.h)
+          float d8[8], g8[8], u8[8], dg[8], du[8];
+          unpack8e<E>(v, d8);
+          unpack8e<E>(g16[q], g8);
+          unpack8e<E>(u16[q], u8);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) swiglu_grad(g8[e], u8[e], d8[e], p.exact, dg[e], du[e]);
+          *reinterpret_cast<uint4*>(p.c + gm * p.ldc + gn) = pack8e<E>(dg);
+          *reinterpret_cast<uint4*>(p.c + gm * p.ldc + p.ffn + gn) = pack8e<E>(du);
+        }
+      }
+    }
+  } else if (cc < 2 * NJ) {
 #pragma unroll 4
     for (int rr = 0; rr < 32; ++rr) {
       const int row = rr * 4 + (lane >> 4);
@@ -552,19 +585,6 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(W4Args p) {
       const long gm = m0 + wm * 128 + row;
       // W4_SWIGLU: wave column half 0 holds g (gu columns [0, F)), half 1 holds u ([F, 2F))
       const int gn = EPI == W4_SWIGLU ? (wn ? p.ffn : 0) + f0 + cc * 8 : n0 + wn * NW + cc * 8;
-      if constexpr (EPI == W4_SWIGLU_BWD) {
-        // v = da (bf16, as the unfused path's GEMM output) for features gn .. gn + 7 of token gm:
-        // dg, du from the saved g = gu[gm, gn], u = gu[gm, F + gn] (swiglu.hip swiglu_grad)
-        float d8[8], g8[8], u8[8], dg[8], du[8];
-        unpack8e<E>(v, d8);
-        unpack8e<E>(*reinterpret_cast<const uint4*>(p.r + gm * p.ldr + gn), g8);
-        unpack8e<E>(*reinterpret_cast<const uint4*>(p.r + gm * p.ldr + p.ffn + gn), u8);
-#pragma unroll
-        for (int q = 0; q < 8; ++q) swiglu_grad(g8[q], u8[q], d8[q], p.exact, dg[q], du[q]);
-        *reinterpret_cast<uint4*>(p.c + gm * p.ldc + gn) = pack8e<E>(dg);
-        *reinterpret_cast<uint4*>(p.c + gm * p.ldc + p.ffn + gn) = pack8e<E>(du);
-        continue;
-      }
       if constexpr (EPI == W4_RES) {
         float a[8], r[8];
         unpack8e<E>(v, a);
