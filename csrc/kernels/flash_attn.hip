@@ -201,6 +201,33 @@ __device__ __forceinline__ float max_lane32(float x) {
   return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
 }
 
+// One output row per lane pair (lanes l and l + 32 hold the same row): lane half hi holds, per
+// (db, g), columns db*32 + 8g + 4hi .. +3 (val(db, 4g + j)). Stored as 16-byte pieces: the halves
+// swap the 4-column halves the other one completes (one v_permlane32_swap per dword), then each
+// lane stores the 8-column chunks of its parity (g even: hi 0, odd: hi 1) — 2 * NDB stores of
+// 16 B instead of 4 * NDB of 8 B (the attention epilogue's store tail is issue-bound). Every
+// lane must call it (the swaps are wave-wide); `ok` guards the stores only.
+template <class E, int NDB, class F>
+__device__ __forceinline__ void store_row16(bf16_t* orow, int hi, bool ok, F val) {
+#pragma unroll
+  for (int db = 0; db < NDB; ++db)
+#pragma unroll
+    for (int gp = 0; gp < 2; ++gp) {
+      const int g0 = 2 * gp, g1 = 2 * gp + 1;
+      uint2 pe, po;  // this lane's 4 columns of chunks g0 / g1
+      pe.x = pk2<E>(val(db, 4 * g0 + 0), val(db, 4 * g0 + 1));
+      pe.y = pk2<E>(val(db, 4 * g0 + 2), val(db, 4 * g0 + 3));
+      po.x = pk2<E>(val(db, 4 * g1 + 0), val(db, 4 * g1 + 1));
+      po.y = pk2<E>(val(db, 4 * g1 + 2), val(db, 4 * g1 + 3));
+      const unsigned sx = hi ? pe.x : po.x, sy = hi ? pe.y : po.y;
+      const auto rx = __builtin_amdgcn_permlane32_swap(sx, sx, false, false);  // [0]: low half, [1]: high
+      const auto ry = __builtin_amdgcn_permlane32_swap(sy, sy, false, false);
+      const unsigned qx = hi ? rx[0] : rx[1], qy = hi ? ry[0] : ry[1];  // the partner's half
+      const uint4 o = hi ? make_uint4(qx, qy, po.x, po.y) : make_uint4(pe.x, pe.y, qx, qy);
+      if (ok) *reinterpret_cast<uint4*>(orow + db * 32 + 8 * (hi ? g1 : g0)) = o;
+    }
+}
+
 // lse2 / delta rows are padded to a multiple of 32 queries, so a 32-query slice's
 // statistics are whole, aligned float4s (padding entries are never used unmasked).
 __host__ __device__ __forceinline__ int stat_stride(int S) { return (S + 31) & ~31; }
@@ -422,19 +449,9 @@ __global__ __launch_bounds__(64 * NW * SPLIT, 8 / (NW * SPLIT)) void flash_fwd_k
 
   l += __shfl_xor(l, 32, 64);
   const float inv = 1.f / l;
-  if (qrow < S) {
-    bf16_t* orow = out + ((long)b * S + qrow) * ldo + (long)h * D;
-#pragma unroll
-    for (int db = 0; db < NDB; ++db)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        uint2 v;
-        v.x = pk2<E>(o[db][4 * g + 0] * inv, o[db][4 * g + 1] * inv);
-        v.y = pk2<E>(o[db][4 * g + 2] * inv, o[db][4 * g + 3] * inv);
-        *reinterpret_cast<uint2*>(orow + db * 32 + 8 * g + 4 * hi) = v;
-      }
-    if (hi == 0) lse2[((long)b * Hq + h) * stat_stride(S) + qrow] = m + log2f(l);
-  }
+  store_row16<E, NDB>(out + ((long)b * S + min(qrow, S - 1)) * ldo + (long)h * D, hi, qrow < S,
+                      [&](int db, int i) { return o[db][i] * inv; });
+  if (qrow < S && hi == 0) lse2[((long)b * Hq + h) * stat_stride(S) + qrow] = m + log2f(l);
 }
 
 // ================================================================== forward, software-pipelined
@@ -653,19 +670,9 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void flash_fwd_pipe_kernel(
 
   l += __shfl_xor(l, 32, 64);
   const float inv = 1.f / l;
-  if (qrow < S) {
-    bf16_t* orow = out + ((long)b * S + qrow) * ldo + (long)h * D;
-#pragma unroll
-    for (int db = 0; db < NDB; ++db)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        uint2 v;
-        v.x = pk2<E>(o[db][4 * g + 0] * inv, o[db][4 * g + 1] * inv);
-        v.y = pk2<E>(o[db][4 * g + 2] * inv, o[db][4 * g + 3] * inv);
-        *reinterpret_cast<uint2*>(orow + db * 32 + 8 * g + 4 * hi) = v;
-      }
-    if (hi == 0) lse2[((long)b * Hq + h) * stat_stride(S) + qrow] = m + log2f(l);
-  }
+  store_row16<E, NDB>(out + ((long)b * S + min(qrow, S - 1)) * ldo + (long)h * D, hi, qrow < S,
+                      [&](int db, int i) { return o[db][i] * inv; });
+  if (qrow < S && hi == 0) lse2[((long)b * Hq + h) * stat_stride(S) + qrow] = m + log2f(l);
 }
 
 // ================================================================== backward
@@ -1301,18 +1308,42 @@ __global__ __launch_bounds__(64 * NW * SPLIT, SPLIT == 1 ? 4 / NW : 8 / (NW * SP
 
   // dK / dV of this q-head in bf16: per-q-head partials [T, Hq*D] (ldkv = Hq*D) that the
   // finalize kernel sums over the GQA group, or — without GQA (Hq == Hkv) — straight into the
-  // K / V columns of dqkv (the pointers are offset by the host, ldkv = its row stride)
+  // K / V columns of dqkv (the pointers are offset by the host, ldkv = its row stride).
+  // Staged through LDS (the pair buffers are free now): a lane holds one column of 16 key rows,
+  // so storing from the accumulators takes 2-byte stores — 128 per lane, the kernel's tail; from
+  // the staged rows every lane stores 16-byte row pieces (8 per array). Rows of D bf16, 16-byte
+  // chunk c of row r at c ^ (r % CH).
+  {
+    constexpr int CH = D / 8;                 // 16-byte chunks per row
+    constexpr int WB = 32 * D * 2 * 2;        // one wave's dK | dV rows
+    constexpr int PB = 2 * SLOT * SPLIT;      // bytes of each pair buffer
+    static_assert(2 * WB <= PB && NW <= 4, "dK/dV staging");
+    __syncthreads();  // every wave is done with the pair buffers (and the SPLIT merge)
+    char* const stg = (wave < 2 ? pb0 : pb1) + (wave & 1) * WB;
+    auto at = [](int r, int d) { return r * (D * 2) + (((d >> 3) ^ (r % CH)) << 4) + (d & 7) * 2; };
 #pragma unroll
-  for (int db = 0; db < NDB; ++db)
+    for (int db = 0; db < NDB; ++db)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int k = kw + (r & 3) + 8 * (r >> 2) + 4 * hi;
+      for (int r = 0; r < 16; ++r) {
+        const int kr = (r & 3) + 8 * (r >> 2) + 4 * hi;
+        const int d = db * 32 + l32;
+        *reinterpret_cast<bf16_t*>(stg + at(kr, d)) = cvt1<E>(dk[db][r] * scale);
+        *reinterpret_cast<bf16_t*>(stg + 32 * D * 2 + at(kr, d)) = cvt1<E>(dv[db][r]);
+      }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's staging writes landed
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int it = 0; it < 32 * CH / 64; ++it) {
+      const int i = it * 64 + lane, r = i / CH, c = i % CH;
+      const int k = kw + r;
       if (k < S) {
-        const long off = ((long)b * S + k) * ldkv + (long)h * D + db * 32 + l32;
-        dk_part[off] = cvt1<E>(dk[db][r] * scale);
-        dv_part[off] = cvt1<E>(dv[db][r]);
+        const int so = r * (D * 2) + ((c ^ (r % CH)) << 4);
+        const long off = ((long)b * S + k) * ldkv + (long)h * D + c * 8;
+        *reinterpret_cast<uint4*>(dk_part + off) = *reinterpret_cast<const uint4*>(stg + so);
+        *reinterpret_cast<uint4*>(dv_part + off) = *reinterpret_cast<const uint4*>(stg + 32 * D * 2 + so);
       }
     }
+  }
 
   if (fold.cnt != nullptr) {
     // (SPLIT = 2: half-block 1 has exited; the barriers count the 64 * NW threads left)
@@ -1527,18 +1558,8 @@ __global__ __launch_bounds__(64 * NW * SPLIT, SPLIT == 1 ? 4 / NW : 8 / (NW * SP
       for (int r = 0; r < 16; ++r) dq[db][r] += xq[(db * 16 + r) * NW * 64];
   }
 
-  if (qrow < S) {
-    bf16_t* orow = dqkv + ((long)b * S + qrow) * ldv + (long)h * D;
-#pragma unroll
-    for (int db = 0; db < NDB; ++db)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        uint2 v;
-        v.x = pk2<E>(dq[db][4 * g + 0] * scale, dq[db][4 * g + 1] * scale);
-        v.y = pk2<E>(dq[db][4 * g + 2] * scale, dq[db][4 * g + 3] * scale);
-        *reinterpret_cast<uint2*>(orow + db * 32 + 8 * g + 4 * hi) = v;
-      }
-  }
+  store_row16<E, NDB>(dqkv + ((long)b * S + min(qrow, S - 1)) * ldv + (long)h * D, hi, qrow < S,
+                      [&](int db, int i) { return dq[db][i] * scale; });
 }
 
 // dqkv[:, q | k | v] = bf16(dQ), bf16(sum_G dK_part), bf16(sum_G dV_part).
