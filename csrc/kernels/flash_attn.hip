@@ -947,13 +947,13 @@ template <class E>
 __device__ __forceinline__ void fin_unit(const float* __restrict__ dq_acc, const bf16_t* __restrict__ dk_part,
                                          const bf16_t* __restrict__ dv_part, bf16_t* __restrict__ dqkv, long t,
                                          int col, int Hq, int Hkv, int D, const float* __restrict__ cos_t,
-                                         const float* __restrict__ sin_t, int S) {
+                                         const float* __restrict__ sin_t, int S, bool q_done = false) {
   const int G = Hq / Hkv;
   const int W = (Hq + 2 * Hkv) * D;
   float4 v;
   if (col < Hq * D) {
     if (dq_acc == nullptr) {  // dQ already written by the deterministic dQ kernel
-      if (cos_t == nullptr) return;
+      if (cos_t == nullptr || q_done) return;  // (q_done: rotated there too)
       const uint2 x = *reinterpret_cast<const uint2*>(dqkv + t * W + col);
       v = make_float4(u16f<E>(x.x), u16f<E>(x.x >> 16), u16f<E>(x.y), u16f<E>(x.y >> 16));
     } else {
@@ -1000,6 +1000,7 @@ struct GqaFold {
   const float* cos_t;      // RoPE tables or null
   const float* sin_t;
   int dbg;                 // timing experiments only (FT_FLASH_FOLD_DBG): 1 no fold work, 2 no release fence
+  int q_done;              // dQ already rotated by the dQ kernel
 };
 
 // The fold of `rows` rows from t0 (one key tile of kv head kvh) by NT threads: 16-B units (8
@@ -1012,7 +1013,7 @@ __device__ __forceinline__ void gqa_fold_rows(const bf16_t* __restrict__ dk_part
                                               int S, int tid) {
   constexpr int U = 4, CU = D / 8;  // units per thread per pass, units per head row
   const long W = (long)(Hq + 2 * Hkv) * D;
-  const int uq = f.cos_t != nullptr ? G * CU : 0;
+  const int uq = f.cos_t != nullptr && !f.q_done ? G * CU : 0;
   const int upr = uq + 2 * CU;
   const int n = rows * upr;
   for (int base = 0; base < n; base += NT * U) {
@@ -1383,7 +1384,8 @@ template <class E, int D, int NW = 4, int SPLIT = 1>
 __global__ __launch_bounds__(64 * NW * SPLIT, SPLIT == 1 ? 4 / NW : 8 / (NW * SPLIT)) void flash_bwd_dq_kernel(
     const bf16_t* __restrict__ dO, const bf16_t* __restrict__ qk, const bf16_t* __restrict__ qkv,
     const float* __restrict__ lse2, float* __restrict__ delta, bf16_t* __restrict__ dqkv, int B,
-    int S, int Hq, int Hkv, float sl2, float scale, long ldqk_, const bf16_t* __restrict__ O) {
+    int S, int Hq, int Hkv, float sl2, float scale, long ldqk_, const bf16_t* __restrict__ O,
+    const float* __restrict__ cos_t, const float* __restrict__ sin_t) {
   constexpr int BM = 32 * NW, BN = 64, KS = D / 16, NDB = D / 32;
   constexpr int TILE = BN * D * 2;
   // K | V tiles arrive by LDS-DMA (no staging VGPRs held across the compute: at one wave
@@ -1558,8 +1560,22 @@ __global__ __launch_bounds__(64 * NW * SPLIT, SPLIT == 1 ? 4 / NW : 8 / (NW * SP
       for (int r = 0; r < 16; ++r) dq[db][r] += xq[(db * 16 + r) * NW * 64];
   }
 
-  store_row16<E, NDB>(dqkv + ((long)b * S + min(qrow, S - 1)) * ldv + (long)h * D, hi, qrow < S,
-                      [&](int db, int i) { return dq[db][i] * scale; });
+  if (cos_t == nullptr) {
+    store_row16<E, NDB>(dqkv + ((long)b * S + min(qrow, S - 1)) * ldv + (long)h * D, hi, qrow < S,
+                        [&](int db, int i) { return dq[db][i] * scale; });
+  } else {
+    // RoPE backward of dQ here (reference model.py:100-126 transposed: the interleaved pair
+    // (x0, x1) times cis(-theta)): a lane's 4 consecutive columns are two whole pairs, so the
+    // rotation is in-lane, in fp32 before the one rounding; the finalize pass skips the Q columns
+    const long pos = min(qrow, S - 1);
+    store_row16<E, NDB>(dqkv + ((long)b * S + pos) * ldv + (long)h * D, hi, qrow < S, [&](int db, int i) {
+      const int i0 = i & ~1;
+      const float a0 = dq[db][i0] * scale, b0 = dq[db][i0 + 1] * scale;
+      const int fi = (db * 32 + 8 * (i >> 2) + 4 * hi + (i & 3)) >> 1;
+      const float c = cos_t[pos * (D / 2) + fi], sn = sin_t[pos * (D / 2) + fi];
+      return (i & 1) ? fmaf(-a0, sn, b0 * c) : fmaf(a0, c, b0 * sn);
+    });
+  }
 }
 
 // dqkv[:, q | k | v] = bf16(dQ), bf16(sum_G dK_part), bf16(sum_G dV_part).
@@ -1572,13 +1588,16 @@ template <class E>
 __global__ __launch_bounds__(256) void flash_bwd_finalize_kernel(
     const float* __restrict__ dq_acc, const bf16_t* __restrict__ dk_part,
     const bf16_t* __restrict__ dv_part, bf16_t* __restrict__ dqkv, long T, int Hq, int Hkv, int D,
-    const float* __restrict__ cos_t, const float* __restrict__ sin_t, int S) {
+    const float* __restrict__ cos_t, const float* __restrict__ sin_t, int S, int q_done) {
   const int W = (Hq + 2 * Hkv) * D;
-  const int vpr = W / 4;
+  // q_done: the dQ columns are final (rotated by the dQ kernel): only the K / V columns remain
+  const int c0 = q_done ? Hq * D / 4 : 0;
+  const int vpr = W / 4 - c0;
   const long total = T * vpr;
   for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
     const long t = i / vpr;
-    fin_unit<E>(dq_acc, dk_part, dv_part, dqkv, t, (int)(i - t * vpr) * 4, Hq, Hkv, D, cos_t, sin_t, S);
+    fin_unit<E>(dq_acc, dk_part, dv_part, dqkv, t, (int)(i - t * vpr + c0) * 4, Hq, Hkv, D, cos_t, sin_t, S,
+                q_done != 0);
   }
 }
 
@@ -1783,8 +1802,13 @@ at::Tensor flash_bwd(const at::Tensor& dout, const at::Tensor& qk, const at::Ten
     const char* e = std::getenv("FT_FLASH_FOLD_DBG");
     return e == nullptr ? 0 : std::atoi(e);
   }();
+  // RoPE backward of dQ in the dQ kernel's epilogue (deterministic mode, GQA partials to fold; the
+  // direct no-GQA path rotates Q and K in one rope_bwd_ pass)
+  const bool q_rot = rope && det && !direct;
+  const float* dq_cos = q_rot ? cptr<float>(*cos_t) : nullptr;
+  const float* dq_sin = q_rot ? cptr<float>(*sin_t) : nullptr;
   GqaFold fold{nullptr, mptr<bf16_t>(dqkv), rope ? cptr<float>(*cos_t) : nullptr,
-               rope ? cptr<float>(*sin_t) : nullptr, fold_dbg};
+               rope ? cptr<float>(*sin_t) : nullptr, fold_dbg, q_rot ? 1 : 0};
   if (use_dkdv2 && !direct && g_bwd_fold)
     fold.cnt = fold_counters(qk.device(), (long)B * Hkv * ((S + 32 * nw_ - 1) / (32 * nw_)));
   const int pre_blocks = (int)((rows * 16 + 255) / 256);
@@ -1818,12 +1842,12 @@ at::Tensor flash_bwd(const at::Tensor& dout, const at::Tensor& qk, const at::Ten
     hipLaunchKernelGGL((flash_bwd_dq_kernel<E, DD, NW_, 2>), grid2, dim3(128 * NW_), 0, ft_stream(),       \
                        cptr<bf16_t>(dout), cptr<bf16_t>(qk), cptr<bf16_t>(qkv), cptr<float>(lse),       \
                        mptr<float>(delta), mptr<bf16_t>(dqkv), B, (int)S, (int)Hq, (int)Hkv, sl2, scale, ldqk, \
-                       cptr<bf16_t>(out));                                                              \
+                       cptr<bf16_t>(out), dq_cos, dq_sin);                                              \
   else                                                                                                  \
     hipLaunchKernelGGL((flash_bwd_dq_kernel<E, DD, NW_, 1>), grid2, block2, 0, ft_stream(),                \
                        cptr<bf16_t>(dout), cptr<bf16_t>(qk), cptr<bf16_t>(qkv), cptr<float>(lse),       \
                        mptr<float>(delta), mptr<bf16_t>(dqkv), B, (int)S, (int)Hq, (int)Hkv, sl2, scale, ldqk, \
-                       cptr<bf16_t>(out))
+                       cptr<bf16_t>(out), dq_cos, dq_sin)
 #define FT_PRE(DD)                                                                                      \
   hipLaunchKernelGGL((flash_bwd_pre_kernel<E, DD>), dim3(pre_blocks), block, 0, ft_stream(),             \
                      cptr<bf16_t>(dout), cptr<bf16_t>(out), mptr<float>(delta), B, (int)S, (int)Hq)
@@ -1866,7 +1890,7 @@ at::Tensor flash_bwd(const at::Tensor& dout, const at::Tensor& qk, const at::Ten
                                      det ? nullptr : cptr<float>(dq_acc), cptr<bf16_t>(dk_part),
                                      cptr<bf16_t>(dv_part), mptr<bf16_t>(dqkv), (long)T, (int)Hq,
                                      (int)Hkv, (int)D, rope ? cptr<float>(*cos_t) : nullptr,
-                                     rope ? cptr<float>(*sin_t) : nullptr, (int)S));
+                                     rope ? cptr<float>(*sin_t) : nullptr, (int)S, q_rot ? 1 : 0));
   FT_LAUNCH_CHECK();
   return dqkv;
 }
