@@ -739,7 +739,11 @@ void launch(at::ScalarType st_, int nj, const W4Args& p, int epi, hipStream_t st
 }
 
 // Tile width for N: whole rounds of 256 tiles where possible (M = 2048 -> 8 row tiles).
-int pick_nj(long M, long N) {
+// kmajor_a (the dW layout, both operands k-major): the 256 x 128 tile is LDS-bound there (16
+// transposed fragment reads per k-step for 32 MFMAs): measured 0.65 of the wide tile's rate per
+// unit of work (8B qkv dW 6144 x 4096 x 2048: 116.4 us at 128 columns in 3 rounds vs 99.9 us at
+// 256 in 2, profiles/r4_w4_dw_nj_probe.log).
+int pick_nj(long M, long N, bool kmajor_a = false) {
   const long tm = M / BM;
   int best = 0;
   double best_cost = 1e30;
@@ -749,7 +753,7 @@ int pick_nj(long M, long N) {
     const long tiles = tm * (N / bn);
     const long rounds = (tiles + 255) / 256;
     // time ~ rounds x tile work; a narrower tile re-reads A more per MFMA (x ~1.06 for 4)
-    const double eff = nj == 8 ? 1.0 : nj == 7 ? 0.99 : nj == 6 ? 0.98 : 0.92;
+    const double eff = nj == 8 ? 1.0 : nj == 7 ? 0.99 : nj == 6 ? 0.98 : (kmajor_a ? 0.65 : 0.92);
     const double cost = (double)rounds * nj / eff;
     if (cost < best_cost - 1e-9) {
       best_cost = cost;
@@ -829,7 +833,7 @@ at::Tensor gemm_w4_ex(const at::Tensor& a, bool a_t, const at::Tensor& b, bool b
   FT_CHECK_CONTIG(a);
   FT_CHECK_CONTIG(b);
   TORCH_CHECK(a.numel() == M * K && b.numel() == N * K, "gemm_w4_ex: operand sizes do not match M, N, K");
-  const int NJ = nj > 0 ? (int)nj : pick_nj(M, N);
+  const int NJ = nj > 0 ? (int)nj : pick_nj(M, N, a_t);
   TORCH_CHECK(NJ == 8 || NJ == 7 || NJ == 6 || NJ == 4, "gemm_w4_ex: no tile width fits N = ", N);
   TORCH_CHECK(M % BM == 0 && N % (32 * NJ) == 0 && K % (2 * BK) == 0 && K > 0, "gemm_w4_ex: M % 256, N % ",
               32 * NJ, ", K % 128 (got ", M, " ", N, " ", K, ")");
