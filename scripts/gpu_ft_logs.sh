@@ -10,13 +10,13 @@ mkdir -p gpurun_out/logs
 S=scripts/gpu_check.sh
 timeout -k 10 300 python -c "import torch; torch.zeros(1, device='cuda')" || exit 1   # page the image in
 CK=/tmp/ftck; rm -rf $CK; mkdir -p $CK
-$S chain_gpt2s 600 python benchmarks/preempt_chain.py --jobs 3 --time 60 --signal-lead 20 --checkpoint-path $CK -- --model gpt2-small --synthetic-data --hip-graph --logging-frequency 100 || exit 1
-mkdir -p gpurun_out/logs/chain_gpt2s && cp /tmp/ftlogs_*/output_*.out gpurun_out/logs/chain_gpt2s/ 2>/dev/null; rm -rf /tmp/ftlogs_*
+$S chain_gpt2s 600 python benchmarks/preempt_chain.py --jobs 3 --time 60 --signal-lead 20 --checkpoint-path $CK --log-dir $PWD/gpurun_out/logs/chain_gpt2s -- --model gpt2-small --synthetic-data --hip-graph --logging-frequency 100 || exit 1
+cp gpurun_out/chain_gpt2s.log gpurun_out/logs/ 2>/dev/null
 rm -rf $CK; mkdir -p $CK
 D=/tmp/ftdata; mkdir -p $D
 python -c "import sys; sys.path.insert(0, 'tests'); from helpers import make_parquet; make_parquet('$D/train.parquet', n_docs=200000, seed=7)" || exit 1
-$S chain_iter 600 python benchmarks/preempt_chain.py --jobs 3 --time 60 --signal-lead 20 --checkpoint-path $CK -- --model gpt2-medium --dataset $D/train.parquet --iterable-dataset --tokenizer-name-or-path byte --vocab-size 131072 --logging-frequency 100 || exit 1
-mkdir -p gpurun_out/logs/chain_iter && cp /tmp/ftlogs_*/output_*.out gpurun_out/logs/chain_iter/ 2>/dev/null; rm -rf /tmp/ftlogs_*
+$S chain_iter 600 python benchmarks/preempt_chain.py --jobs 3 --time 60 --signal-lead 20 --checkpoint-path $CK --log-dir $PWD/gpurun_out/logs/chain_iter -- --model gpt2-medium --dataset $D/train.parquet --iterable-dataset --tokenizer-name-or-path byte --vocab-size 131072 --logging-frequency 100 || exit 1
+cp gpurun_out/chain_iter.log gpurun_out/logs/ 2>/dev/null
 rm -rf $CK; mkdir -p $CK
 W=$PWD/gpurun_out/ftwd; mkdir -p $W
 printf '#!/bin/bash\necho "$@" >> %s/sbatch_calls.txt\necho "Submitted batch job 777"\n' $W > $W/sbatch; chmod +x $W/sbatch
