@@ -356,11 +356,31 @@ class GradReducer:
 
     def _sumsq(self, g: torch.Tensor, b: Bucket) -> None:
         if self.fused_sumsq:
-            # per sink: only gradients whose producer did not write its partials this step
+            # per sink: only gradients whose producer did not write its partials this step. Runs of
+            # such sinks adjacent in the flat buffer, whose partial slices are adjacent too (slices
+            # are assigned in descending address order), take one launch over the whole run: the
+            # small models (no producer partials) issued one tiny sumsq kernel per weight
+            todo = [sk for sk in self._bucket_sq_sinks[b.idx] if not sk.sq_done]
             for sink in self._bucket_sq_sinks[b.idx]:
-                if not sink.sq_done:
-                    kernels().sumsq_into_(sink.buf.reshape(-1), self._sq_slice_of[id(sink)])
                 sink.sq_done = False
+            grads = self.flat.grads
+            base = self.partials.storage_offset()
+            runs = []  # [lo, hi, p_lo, p_hi]
+            for sk in sorted(todo, key=lambda x: x.start):
+                sl = self._sq_slice_of[id(sk)]
+                plo = sl.storage_offset() - base
+                phi = plo + sl.numel()
+                flat_view = sk.buf.data_ptr() == grads.data_ptr() + sk.start * grads.element_size()
+                if (runs and flat_view and runs[-1][1] == sk.start and runs[-1][2] == phi
+                        and runs[-1][3] - plo <= 65535 and runs[-1][4]):
+                    runs[-1][1], runs[-1][2] = sk.end, plo
+                else:
+                    runs.append([sk.start, sk.end, plo, phi, flat_view, sk])
+            for lo, hi, plo, phi, fv, sk in runs:
+                if fv:
+                    kernels().sumsq_into_(grads[lo:hi], self.partials[plo:phi])
+                else:
+                    kernels().sumsq_into_(sk.buf.reshape(-1), self._sq_slice_of[id(sk)])
             return
         part = self.partials[b.part_lo : b.part_hi]
         if native(g):

@@ -127,3 +127,46 @@ def test_fused_sumsq_partials(gates, monkeypatch):
         got = red.global_sumsq().double().sum().item()
         assert abs(got - want) <= 2e-5 * want, (it, got, want)
         assert calls == [], calls
+
+
+def test_fused_sumsq_fallback_runs_merged(monkeypatch):
+    """Without producer partials (the hipBLASLt backward, as for the small presets) every sink
+    falls back to the sum-of-squares pass: adjacent sinks of a bucket take one launch, the total
+    still equals the gradient's sum of squares."""
+    from fault_tolerant_llm_training_amd.models.llama import build_model
+    from fault_tolerant_llm_training_amd.ops import functional as Fx
+    from fault_tolerant_llm_training_amd.parallel import ddp
+
+    monkeypatch.setattr(Fx, "_W4_BWD", False)
+    calls = []
+    real = ddp.kernels()
+
+    class Spy:
+        def __getattr__(self, n):
+            f = getattr(real, n)
+            if n == "sumsq_into_":
+                def g(grad, part):
+                    calls.append(grad.numel())
+                    return f(grad, part)
+                return g
+            return f
+
+    monkeypatch.setattr(ddp, "kernels", lambda: Spy())
+    a = _args()
+    m = build_model(a, "cuda", torch.bfloat16, seed=3)
+    red = ddp.GradReducer(m.flat, m.sinks_in_backward_order(), bucket_mb=1.0)
+    assert red.fused_sumsq
+    torch.manual_seed(1)
+    tok = torch.randint(0, a.vocab_size, (1, a.seq_len), device="cuda")
+    for it in range(2):
+        calls.clear()
+        red.begin_micro(0, 1)
+        m(tok, tok).backward()
+        red.finish()
+        torch.cuda.synchronize()
+        want = m.flat.grads.double().pow(2).sum().item()
+        got = red.global_sumsq().double().sum().item()
+        assert abs(got - want) <= 2e-5 * want, (it, got, want)
+        fallback = [s for s in red._sq_sinks if s.part is not None]
+        assert 0 < len(calls) < len(fallback), (len(calls), len(fallback))
+        assert sum(calls) <= m.flat.grads.numel()
