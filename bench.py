@@ -12,8 +12,11 @@ reduce-scatter by default for N > 1; ``--dp-mode allreduce`` for replicated
 state), gradient norm + clip, AdamW (+ parameter all-gather under ZeRO-1),
 LR-scheduler step.
 
-    python bench.py --gpus N --steps K --warmup W
+    python bench.py --gpus N --steps K --warmup W       (N > 1: starts N ranks itself, see self_launch)
     torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU)
+
+The process group's size must equal ``--gpus`` (exit 2 otherwise), so an N-GPU row is always an
+N-rank measurement.
 
 Rank 0 prints one JSON line; ``value`` is the whole-job tokens/s (sum over
 GPUs, the driver's contract), timed between barriers + device syncs, max step
@@ -82,8 +85,58 @@ def _sync(dev):
         torch.cuda.synchronize(dev)
 
 
+def _launched_world():
+    """WORLD_SIZE of the launcher this process runs under (torchrun or Slurm), or None."""
+    env = os.environ
+    if "WORLD_SIZE" in env:
+        return int(env["WORLD_SIZE"])
+    if "SLURM_NTASKS" in env and "SLURM_PROCID" in env:
+        return int(env["SLURM_NTASKS"])
+    return None
+
+
+def _free_port() -> int:
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def self_launch(a) -> int | None:
+    """``--gpus N`` (N > 1) with no launcher: start N ranks as a child torchrun and return its exit
+    code, so the N-GPU row can never be a 1-rank number. Runs before anything touches the GPU
+    (``torch.cuda.device_count`` does not initialise HIP on this image); the child is a separate
+    process, never an exec. Returns None when this process is already one rank of a launch."""
+    world = _launched_world()
+    if world is not None or a.gpus <= 1:
+        return None
+    if a.device == "cuda":
+        have = torch.cuda.device_count()
+        if have < a.gpus:
+            print(f"[bench] --gpus {a.gpus} but only {have} GPU(s) visible", file=sys.stderr)
+            return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(a.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    print(f"[bench] no launcher: starting {a.gpus} ranks ({' '.join(cmd[1:6])} ...)", file=sys.stderr, flush=True)
+    import subprocess
+
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     a = parse()
+    rc = self_launch(a)
+    if rc is not None:
+        sys.exit(rc)
+    launched = _launched_world()
+    if launched is not None and launched != a.gpus:
+        print(f"[bench] --gpus {a.gpus} but the launcher started {launched} rank(s)", file=sys.stderr)
+        sys.exit(2)
     from fault_tolerant_llm_training_amd.parallel import dist as fdist
     from fault_tolerant_llm_training_amd.parallel.ddp import GradReducer
     from fault_tolerant_llm_training_amd.models.llama import build_model, model_args_for, flops_per_token
@@ -100,11 +153,9 @@ def main():
         # optimizer/snapshot side streams when both have work queued
         torch.cuda.set_stream(torch.cuda.Stream(device=dev, priority=-1))
     world = info.world_size
-    if a.gpus != world and info.is_main:
-        print(f"[bench] note: --gpus {a.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
-    # what the job really runs on: process-group size, one distinct GPU per rank (raises
-    # otherwise), peer access between every pair, RCCL version -- recorded in the JSON line
-    topo = fdist.topology_report(info, expected_world=a.gpus if world > 1 else None)
+    # what the job really runs on: process-group size (must be --gpus), one distinct GPU per rank
+    # (raises otherwise), peer access between every pair, RCCL version -- recorded in the JSON line
+    topo = fdist.topology_report(info, expected_world=a.gpus)
 
     margs = model_args_for(a.model, vocab_size=a.vocab_size, seq_len=a.seq_len)
     model = build_model(margs, dev, torch.bfloat16, seed=1234)

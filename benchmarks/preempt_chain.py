@@ -77,8 +77,9 @@ def main():
     ap.add_argument("--checkpoint-path", default="")
     ap.add_argument("--log-dir", default="", help="where the jobs' output_<JOBID>.out go (default: a temp dir)")
     ap.add_argument("--prune-consumed", action="store_true",
-                    help="delete a job's checkpoint once the next job has resumed from it (an 8B chain "
-                         "holds one 48 GB checkpoint on disk at a time instead of one per job)")
+                    help="delete a job's checkpoint once the next job has resumed from it AND written a "
+                         "durable checkpoint of its own (an 8B chain holds at most two 48 GB checkpoints "
+                         "on disk instead of one per job, and always one it can resume from)")
     ap.add_argument("train_args", nargs=argparse.REMAINDER)
     a = ap.parse_args()
     extra = [x for x in a.train_args if x != "--"]
@@ -94,16 +95,21 @@ def main():
     pruned = []
 
     def prune(rec):
-        # the running job has loaded its predecessor's checkpoint: that file is no longer needed
+        # the running job resumed from its predecessor's checkpoint and has since made its own
+        # durable (a periodic save's "Checkpoint written" or the exit handler's "Checkpoint saved",
+        # both logged after the atomic rename): only then is the predecessor's file not needed --
+        # a job that dies before its first save is resumed from the predecessor's again
         if not sim.jobs or sim.jobs[-1].job_id in pruned:
             return
         prev = sim.jobs[-1].job_id
         try:
             with open(rec.log) as f:
-                resumed = "Resuming training from training_step" in f.read()
+                text = f.read()
         except OSError:
             return
-        if resumed:
+        resumed = "Resuming training from training_step" in text
+        own = "Checkpoint written:" in text or "[EXIT HANDLER] Checkpoint saved at step" in text
+        if resumed and own:
             path = checkpoint_file(ck, prev)
             if os.path.exists(path):
                 os.remove(path)

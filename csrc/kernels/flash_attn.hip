@@ -1809,7 +1809,9 @@ at::Tensor flash_bwd(const at::Tensor& dout, const at::Tensor& qk, const at::Ten
   const float* dq_sin = q_rot ? cptr<float>(*sin_t) : nullptr;
   GqaFold fold{nullptr, mptr<bf16_t>(dqkv), rope ? cptr<float>(*cos_t) : nullptr,
                rope ? cptr<float>(*sin_t) : nullptr, fold_dbg, q_rot ? 1 : 0};
-  if (use_dkdv2 && !direct && g_bwd_fold)
+  // the in-kernel fold holds at most 8 q-head partials per unit (uint4 x[U][8]): wider groups
+  // take the finalize pass
+  if (use_dkdv2 && !direct && g_bwd_fold && Hq / Hkv <= 8)
     fold.cnt = fold_counters(qk.device(), (long)B * Hkv * ((S + 32 * nw_ - 1) / (32 * nw_)));
   const int pre_blocks = (int)((rows * 16 + 255) / 256);
   const int nkt = (S + 127) / 128;

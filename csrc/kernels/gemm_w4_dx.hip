@@ -1,0 +1,10 @@
+// w4 GEMM instantiations: K-contiguous A, k-major B (dX).
+#include "gemm_w4.h"
+
+namespace ftw4 {
+
+void launch_dx(at::ScalarType st_, int nj, const W4Args& p, int epi, hipStream_t st) {
+  launch_l<false, true>(st_, nj, p, epi, st);
+}
+
+}  // namespace ftw4

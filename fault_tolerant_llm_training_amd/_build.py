@@ -83,6 +83,23 @@ def _common_flags(ext_name: str):
     ]
 
 
+def _includes(src: Path, dirs, seen=None):
+    """Local headers ``src`` includes (``#include "x.h"``), transitively."""
+    seen = set() if seen is None else seen
+    for line in src.read_text(errors="replace").splitlines():
+        line = line.strip()
+        if not line.startswith("#include \""):
+            continue
+        name = line.split('"')[1]
+        for d in dirs:
+            h = d / name
+            if h.exists() and h not in seen:
+                seen.add(h)
+                _includes(h, dirs, seen)
+                break
+    return seen
+
+
 def _needs(obj: Path, src: Path, headers) -> bool:
     if not obj.exists():
         return True
@@ -92,15 +109,42 @@ def _needs(obj: Path, src: Path, headers) -> bool:
     return any(h.stat().st_mtime > t for h in headers)
 
 
+# The w4 GEMM translation units: their device assembly is kept (-save-temps=obj, the exact code
+# that is assembled and linked) and checked by _w4check before _kernels.so may be linked.
+W4_CHECKED = ("gemm_w4_fwd", "gemm_w4_dx", "gemm_w4_dw")
+
+
+def _asm_of(src: Path, obj: Path) -> Path:
+    return obj.parent / f"{src.stem}-hip-amdgcn-amd-amdhsa-{ARCH}.s"
+
+
 def _compile(src: Path, obj: Path, flags, device: bool):
     cmd = [_hipcc()] + flags
     if device:
         cmd += [f"--offload-arch={ARCH}", "-x", "hip"]
+        if src.stem in W4_CHECKED:
+            cmd += ["-save-temps=obj"]
     cmd += ["-c", str(src), "-o", str(obj)]
-    r = subprocess.run(cmd, capture_output=True, text=True)
+    r = subprocess.run(cmd, capture_output=True, text=True, cwd=str(obj.parent))
     if r.returncode != 0:
         raise RuntimeError(f"compile failed: {src}\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    if device and src.stem in W4_CHECKED:
+        check_w4_asm(_asm_of(src, obj), obj)
     return obj
+
+
+def check_w4_asm(asm: Path, obj: Path = None) -> int:
+    """The w4 static check (_w4check) on one TU's kept assembly; on an unsafe placement the object
+    is deleted (so the next build recompiles it) and the build fails. Returns the kernel count."""
+    from . import _w4check
+
+    n, bad = _w4check.check_asm(str(asm))
+    if bad or n == 0:
+        if obj is not None and obj.exists():
+            obj.unlink()
+        raise RuntimeError(f"w4 static check failed for {Path(asm).name} (_kernels.so not linked):\n"
+                           + _w4check.report(n, bad))
+    return n
 
 
 def _link(objs, out: Path, device: bool, extra=()):
@@ -137,13 +181,13 @@ def build(jobs: int = 0, force: bool = False, verbose: bool = True) -> None:
         (RUNTIME_SO, sorted((CSRC / "runtime").glob("*.cpp")), CSRC / "runtime", "_runtime", False, ("-lz", "-ltorch_python")),
     ]
     for out, srcs, hdr_dir, name, device, extra in targets:
-        headers = list(hdr_dir.glob("*.h")) + list((CSRC / "kernels").glob("*.h"))
+        dirs = [hdr_dir, CSRC / "kernels"]
         flags = _common_flags(name)
         objs, work = [], []
         for s in srcs:
             o = BUILD / f"{name}_{s.stem}.o"
             objs.append(o)
-            if force or _needs(o, s, headers):
+            if force or _needs(o, s, _includes(s, dirs)):
                 work.append((s, o))
         if work:
             with cf.ThreadPoolExecutor(max_workers=jobs) as ex:

@@ -21,6 +21,7 @@ LM head model.py:379, loss train.py:101-102.
 from __future__ import annotations
 
 import collections
+import functools
 import os
 from typing import Optional
 
@@ -195,19 +196,31 @@ def _w4t_fits(M: int, N: int, K: int, *ts) -> bool:
     return 0 < nj and (M // 256) * (N // (32 * nj)) >= _W4_MIN_TILES
 
 
-# dX products with a deep reduction (N >= FT_W4_DX_DEEP_K, default 16384: the 8B w13 dX, N = 2F =
-# 28672, and the LM-head dX, N = V) that fill the chip in one round of narrow tiles stay on
-# hipBLASLt: with 256 x 128 tiles the w4 loop is LDS-bound (48 KB of DMA + 96 KB of fragment reads
-# per K-tile per CU for 32 MFMAs per wave), 0.88-0.90x of hipBLASLt on the row-major operands
-# (profiles/r4_gemm_w4t_bench.log); the wider tiles leave half the CUs idle.
-_W4_DX_DEEP_K = int(os.environ.get("FT_W4_DX_DEEP_K", "16384"))
+# dX products with a deep reduction (N >= 16384: the 8B w13 dX, N = 2F = 28672, and the LM-head
+# dX, N = V) whose 256-wide tiles fill only half the chip run split-K on the w4 kernel (each tile's
+# two K halves on two workgroups, gemm_w4.h): with 256 x 128 tiles instead the loop is LDS-bound
+# (0.88-0.90x of hipBLASLt, profiles/r4_gemm_w4t_bench.log). Without a split (FT_W4_SPLITK=0)
+# they go back to hipBLASLt.
+_W4_DX_DEEP_K = 16384
+
+
+@functools.lru_cache(maxsize=256)
+def _w4_plan(M: int, N: int, K: int, a_t: bool, b_t: bool):
+    """(tile width / 32, splits) of the w4 kernel's automatic plan for C[M, N] over K."""
+    return tuple(kernels().gemm_w4_plan(M, N, K, a_t, b_t))
+
+
+def set_w4_splitk(mode: int) -> None:
+    """Split-K of the w4 kernel (FT_W4_SPLITK): 0 off, 1 automatic (default), 2 forced where it fits."""
+    kernels().gemm_w4_set_splitk(int(mode))
+    _w4_plan.cache_clear()
 
 
 def _w4_dx_ok(T: int, K: int, N: int, dy2: torch.Tensor, w: torch.Tensor) -> bool:
     if not (_w4t_fits(T, K, N, dy2, w) and w.is_contiguous()):
         return False
     if N >= _W4_DX_DEEP_K and (T // 256) * (K // 256) <= 256:
-        return False
+        return _w4_plan(T, K, N, False, True)[1] > 1
     return True
 
 

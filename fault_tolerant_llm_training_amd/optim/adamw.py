@@ -189,7 +189,8 @@ class FlatAdamW(torch.optim.Optimizer):
             if native(f.grads):
                 kernels().grad_norm_(f.grads, self.stats, self.max_grad_norm)
             else:
-                _norm_reference(f.grads.float().pow(2).sum().reshape(1), self.stats, self.max_grad_norm)
+                gd = f.grads.double() if f.grads.dtype == torch.float64 else f.grads.float()
+                _norm_reference(gd.pow(2).sum().reshape(1), self.stats, self.max_grad_norm)
             self._update(f.params, f.grads, self.exp_avg, self.exp_avg_sq, lr, b1, b2, eps, wd)
             self._publish_stats()
             return None
@@ -411,14 +412,16 @@ def _norm_reference(sumsq: torch.Tensor, stats: torch.Tensor, max_norm: float) -
 
 
 def _adamw_reference(p, g, m, v, stats, lr, b1, b2, eps, wd, step):
-    """CPU reference of the fused kernel (fp32 math, storage dtype rounding)."""
+    """Reference of the fused kernel (fp32 math, storage dtype rounding); fp64 parameters (the
+    composed path of --model-dtype fp64) are updated in fp64, as the reference's torch AdamW does."""
     if stats[2].item() != 0:
         return
     coef = stats[1].item()
-    gf = g.float() * coef
-    pf = p.float() * (1 - lr * wd)
-    mf = m.float()
-    vf = v.float()
+    md = torch.float64 if p.dtype == torch.float64 else torch.float32
+    gf = g.to(md) * coef
+    pf = p.to(md) * (1 - lr * wd)
+    mf = m.to(md)
+    vf = v.to(md)
     mf.add_((gf - mf) * (1 - b1))
     vf.mul_(b2).add_((1 - b2) * gf * gf)
     bc1 = 1 - b1 ** step

@@ -387,7 +387,7 @@ class GradReducer:
             kernels().sumsq_into_(g, part)
         else:
             part.zero_()
-            part[0] = g.float().pow(2).sum()
+            part[0] = (g.double() if g.dtype == torch.float64 else g.float()).pow(2).sum()
 
     def _launch(self, b: Bucket) -> None:
         if self.cuda:

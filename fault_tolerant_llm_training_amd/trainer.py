@@ -271,7 +271,8 @@ def train(args) -> int:
         # on one GPU without gradient accumulation --compile turns it on. Elsewhere the graph
         # cannot capture the step (collectives / host-side accumulation), so the flag is accepted
         # and logged as not applied.
-        if device.type == "cuda" and not info.distributed and max(1, int(args.grad_accum)) == 1:
+        graphable = model_dtype in (torch.bfloat16, torch.float16, torch.float32)
+        if device.type == "cuda" and not info.distributed and max(1, int(args.grad_accum)) == 1 and graphable:
             logger.info("Using `torch.compile`")
             logger.info("`torch.compile` -> whole-step HIP graph capture (--hip-graph): the step's "
                         "kernel launches are recorded once and replayed")
@@ -279,7 +280,8 @@ def train(args) -> int:
         else:
             logger.info("Using `torch.compile` — accepted for CLI compatibility, not applied: the step "
                         "already runs fused gfx950 kernels and the whole-step HIP graph needs one GPU "
-                        "without gradient accumulation")
+                        "without gradient accumulation, in a dtype the HIP kernels run (bf16/fp16/fp32: "
+                        "the fp64 composed path synchronises with the host inside the step)")
     model.train()
 
     # AdamW moments default to the model dtype like the reference, except under fp16: the second
@@ -512,8 +514,10 @@ def train(args) -> int:
 
     graphed = None
     if args.hip_graph:
-        if info.distributed or K > 1 or device.type != "cuda":
-            raise ValueError("--hip-graph: one GPU without a process group, --grad-accum 1, --device cuda")
+        if info.distributed or K > 1 or device.type != "cuda" \
+                or model_dtype not in (torch.bfloat16, torch.float16, torch.float32):
+            raise ValueError("--hip-graph: one GPU without a process group, --grad-accum 1, --device cuda, "
+                             "--model-dtype bf16/fp16/fp32")
         from .graphs import GraphedStep
 
         inv_dev = torch.empty(1, dtype=torch.float32, device=device)  # static input of the graph

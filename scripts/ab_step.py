@@ -131,7 +131,7 @@ def main():
                "w4bwd": lambda on: (torch.cuda.synchronize(), Fx.set_w4_bwd(on)),
                "psums": lambda on: (torch.cuda.synchronize(), red.set_producer_sums(on)),
                "w4head": lambda on: (torch.cuda.synchronize(), Fx.set_w4_head(on)),
-               "deepdx": lambda on: (torch.cuda.synchronize(), setattr(Fx, "_W4_DX_DEEP_K", 16384 if on else 1 << 40)),
+               "splitk": lambda on: (torch.cuda.synchronize(), Fx.set_w4_splitk(1 if on else 0)),
                "w4dwside": lambda on: (torch.cuda.synchronize(), setattr(Fx, "_W4_DW_SIDE", on)),
                "r4": lambda on: (torch.cuda.synchronize(), Fx.set_w4_bwd(on), red.set_producer_sums(on),
                                  Fx.set_w4_head(on)),

@@ -115,3 +115,27 @@ def test_bench_torchrun_n_ranks_zero1(world, tmp_path):
     assert j["world_size"] == world and len(j["device_ids"]) == world
     assert j["distinct_devices"] >= 1 and "peer_access_all_pairs" in j and "rccl_version" in j
     _check_ckpt(j, world)
+
+
+def test_bench_self_launch_without_launcher(tmp_path):
+    """``python bench.py --gpus 4`` with no torchrun / Slurm variables starts 4 ranks itself (a child
+    torchrun, never an exec) and reports a 4-rank measurement."""
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "4", "--no-ckpt", "--no-exposed-comm"] + ARGS, cwd=ROOT,
+                       env=_env(tmp_path), capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1, r.stdout
+    j = lines[0]
+    assert j["n_gpus"] == 4 and j["world_size"] == 4 and j["config"]["parallelism"] == "dp4"
+    assert len(j["device_ids"]) == 4
+
+
+def test_bench_world_mismatch_fails():
+    """A launcher that started a different number of ranks than ``--gpus`` is an error (rc != 0),
+    never a silently relabelled number."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "3", "--no-ckpt"] + ARGS
+    r = subprocess.run(cmd, cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0
+    assert not _json_lines(r.stdout)
+    assert "launcher started 2" in r.stderr

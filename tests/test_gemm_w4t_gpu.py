@@ -83,7 +83,7 @@ def test_accumulate_and_sumsq(a_t):
     K().gemm_w4_ex(a, a_t, b, True, M, N, Kd, c, True, part, 0)
     assert rel(c, ref + c0) < 4e-3
     # one partial per tile, the sum of squares of exactly the stored (rounded) values
-    assert torch.all(part[tiles:] == -1.0)
+    assert torch.all(part[tiles:] == 0.0)  # slots past the tile grid are zeroed (no stale partials)
     want = c.float().pow(2).sum().item()
     got = part[:tiles].double().sum().item()
     assert abs(got - want) <= 1e-5 * want, (got, want)
@@ -143,3 +143,61 @@ def test_llama8b_products(a_t, M, N, Kd):
     out = K().gemm_w4_ex(a, a_t, b, True, M, N, Kd, None, False, None, 0)
     ref = (a.float().t() if a_t else a.float()) @ b.float()
     assert rel(out, ref) < 4e-3
+
+
+# ---- split-K (gemm_w4.h W4Args::splits): the two halves of K of a tile on two workgroups, the
+# first half's fp32 partial added by the second in its epilogue (fixed order: deterministic)
+@pytest.mark.parametrize("layout", ["fwd", "dx"])
+@pytest.mark.parametrize("nj,M,N,Kd", [(8, 512, 512, 512), (8, 256, 768, 2048), (4, 512, 384, 1024),
+                                       (7, 256, 448, 768)])
+def test_split_k_exact_and_deterministic(layout, nj, M, N, Kd):
+    torch.manual_seed(M + N + Kd + nj)
+    a = ints(M, Kd)
+    if layout == "fwd":
+        b = ints(N, Kd)  # [N, K]: C = A B^T
+        ref = a.float() @ b.float().t()
+        run = lambda sp, out=None, acc=False: K().gemm_nt_w4(a, b, out, out if acc else None, nj, sp)  # noqa: E731
+    else:
+        b = ints(Kd, N)  # stored [K, N]: C = A B
+        ref = a.float() @ b.float()
+        run = lambda sp, out=None, acc=False: K().gemm_w4_ex(a, False, b, True, M, N, Kd, out, acc, None, nj, sp)  # noqa: E731
+    c1, c2 = run(1), run(2)
+    assert torch.equal(c2.float(), ref.bfloat16().float())  # integer sums: exact whatever the split
+    assert torch.equal(c1, c2)
+    # random operands: within bf16 rounding of fp32, and bitwise the same on every launch
+    a.copy_(rnd(M, Kd))
+    b.copy_(rnd(*b.shape))
+    ref = a.float() @ (b.float().t() if layout == "fwd" else b.float())
+    outs = [run(2) for _ in range(3)]
+    assert rel(outs[0], ref) < 4e-3
+    for o in outs[1:]:
+        assert torch.equal(o, outs[0])
+    # residual / accumulate epilogue on the split path
+    c = rnd(M, N)
+    c0 = c.float().clone()
+    run(2, c, True)
+    assert rel(c, ref + c0) < 4e-3
+
+
+def test_split_k_plan_for_the_8b_dx_products():
+    """The automatic plan splits the 8B dX products whose 256-wide tiles fill half the chip (N_out =
+    4096 at M = 2048) and leaves the others alone."""
+    T, D, F, V = 2048, 4096, 14336, 131072
+    plan = lambda M, N, Kd, at=False, bt=True: list(K().gemm_w4_plan(M, N, Kd, at, bt))  # noqa: E731
+    assert plan(T, D, 2 * F) == [8, 2]      # w13 dX
+    assert plan(T, D, V) == [8, 2]          # LM-head dX
+    assert plan(V, D, T, True, True)[1] == 1   # dW: never split
+    assert plan(T, F, D)[1] == 1            # w2 dX: 512 tiles already
+
+
+def test_split_k_8b_head_dx_vs_fp32():
+    """The LM-head dX at the 8B shape (K = 131072 split in two halves of 65536) vs fp32."""
+    torch.manual_seed(9)
+    M, N, Kd = 2048, 4096, 131072
+    a = rnd(M, Kd)
+    b = rnd(Kd, N)
+    c = K().gemm_w4_ex(a, False, b, True, M, N, Kd, None, False, None, 8, 2)
+    rows = torch.arange(0, M, 97, device="cuda")
+    ref = a[rows].float() @ b.float()
+    assert rel(c[rows], ref) < 4e-3
+    assert torch.equal(c, K().gemm_w4_ex(a, False, b, True, M, N, Kd, None, False, None, 8, 2))

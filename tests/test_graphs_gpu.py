@@ -136,3 +136,21 @@ def test_train_py_compile_is_the_hip_graph_and_resumes_bit_exact(tmp_path):
         for key in ("exp_avg", "exp_avg_sq", "step"):
             assert torch.equal(a["optimizer"]["state"][i][key], b["optimizer"]["state"][i][key]), (i, key)
     assert a["lr_scheduler"] == b["lr_scheduler"]
+
+
+def test_train_py_compile_fp64_runs_eager(tmp_path):
+    """--compile --model-dtype fp64 (both accepted by the reference, train.py:61-63, utils.py:14-19):
+    the fp64 composed path syncs with the host inside the step, so no HIP graph is captured; the
+    run trains eagerly to completion with the reference's log line."""
+    import os
+
+    from helpers import run_train, write_fake_sbatch
+
+    d = str(tmp_path)
+    write_fake_sbatch(d)
+    args = ["--device", "cuda", "--model", "tiny", "--synthetic-data", "--vocab-size", "256",
+            "--sequence-length", "64", "--batch-size", "1", "--model-dtype", "fp64", "--compile",
+            "--logging-frequency", "2", "--checkpoint-path", os.path.join(d, "ck"), "--training-steps", "4"]
+    rc, out = run_train(d, "790", args, timeout=240)
+    assert rc == 0 and "Using `torch.compile`" in out and "not applied" in out, out[-3000:]
+    assert "HIP graph:" not in out and "Training completed" in out, out[-3000:]

@@ -4,9 +4,9 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path.insert(0, os.path.join(ROOT, "scripts"))
+sys.path.insert(0, ROOT)
 
-import w4_asm_check as chk  # noqa: E402
+from fault_tolerant_llm_training_amd import _w4check as chk  # noqa: E402
 
 
 def _asm(body_loop, after_loop, cmp_then_asm=False):
@@ -55,3 +55,25 @@ def test_accumulator_copy_inside_the_loop():
 def test_accumulator_read_before_the_drain():
     e = _errs(_asm([], ["\tv_accvgpr_read_b32 v130, a3"]))
     assert any("before drain" in x for x in e), e
+
+
+def test_scratch_in_the_loop_is_unsafe():
+    lines = _asm(["\tscratch_store_dword off, v7, off"], [])
+    (name, a, b), = list(chk.kernels(lines))
+    e = chk.check(name, lines, a, b, {name: 4})
+    assert any("scratch in the K loop" in x for x in e), e
+
+
+def test_accumulator_spill_before_the_drain_is_unsafe():
+    lines = _asm([], ["\tscratch_store_dwordx4 off, a[4:7], off"])
+    (name, a, b), = list(chk.kernels(lines))
+    e = chk.check(name, lines, a, b, {name: 16})
+    assert any("accumulator spilled before the drain" in x for x in e), e
+
+
+def test_scratch_after_the_drain_is_allowed():
+    lines = _asm([], [])
+    i = next(k for k, l in enumerate(lines) if "v_accvgpr_read_b32 v4, a0" in l)
+    lines.insert(i, "\tscratch_store_dwordx4 off, a[0:3], off")
+    (name, a, b), = list(chk.kernels(lines))
+    assert chk.check(name, lines, a, b, {name: 16}) == []

@@ -170,3 +170,29 @@ def test_fused_sumsq_fallback_runs_merged(monkeypatch):
         fallback = [s for s in red._sq_sinks if s.part is not None]
         assert 0 < len(calls) < len(fallback), (len(calls), len(fallback))
         assert sum(calls) <= m.flat.grads.numel()
+
+
+def test_fused_sumsq_fallback_then_producer(gates):
+    """A step whose sinks took the fallback pass (producer partials off: every slot of a sink's slice
+    written) followed by steps with the w4 dW epilogue partials (fewer tiles than slots): the slots
+    past the tile grid must not keep the fallback's values, or the global norm is inflated."""
+    from fault_tolerant_llm_training_amd.models.llama import build_model
+    from fault_tolerant_llm_training_amd.parallel import ddp
+
+    a = _args()
+    m = build_model(a, "cuda", torch.bfloat16, seed=3)
+    red = ddp.GradReducer(m.flat, m.sinks_in_backward_order(), bucket_mb=1.0)
+    assert red.fused_sumsq
+    torch.manual_seed(2)
+    for it, producers in enumerate([False, True, True]):
+        torch.cuda.synchronize()
+        red.set_producer_sums(producers)
+        tok = torch.randint(0, a.vocab_size, (1, a.seq_len), device="cuda")
+        red.begin_micro(0, 1)
+        # a loss scale that changes per step, so a stale partial cannot match by accident
+        (m(tok, tok) * (1.0 + 3 * it)).backward()
+        red.finish()
+        torch.cuda.synchronize()
+        want = m.flat.grads.double().pow(2).sum().item()
+        got = red.global_sumsq().double().sum().item()
+        assert abs(got - want) <= 2e-5 * want, (it, producers, got, want)
