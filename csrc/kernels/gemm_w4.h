@@ -196,14 +196,14 @@ struct W4Args {
   bf16_t* act;           // a
   bf16_t* actT;          // a^T (null: not written)
   int exact;             // IEEE division in the sigmoid (FT_EXACT_MATH), as swiglu_fwd_t
-  // split-K (W4_STORE / W4_RES, K-contiguous A): splits = 2 runs each output tile as two
-  // workgroups over the two halves of K (grid = 2 x tiles). The first half parks its fp32
-  // accumulators in ws (fragment order: [tile][wave][i][j][lane] float4, 1 KiB per wave store)
-  // and raises flag tick[tile]; the second adds them to its own in the epilogue (fixed order:
-  // deterministic) and re-arms the flag to 0 for the next launch.
+  // split-K (W4_STORE / W4_RES, K-contiguous A): splits = S in 2 .. 8 runs each output tile as
+  // S workgroups over S slices of K (grid = S x tiles, slice-major). Slices 0 .. S-2 park their
+  // fp32 accumulators in ws (fragment order: [tile][slice][wave][i][j][lane] float4, 1 KiB per
+  // wave store) and raise flag tick[8 tile + slice]; the last slice adds them in slice order to
+  // its own in the epilogue (fixed order: deterministic) and re-arms the flags for the next launch.
   int splits;
-  int* tick;             // [tiles] int32, zero between launches (per device and stream)
-  float* ws;             // [tiles * 256 * BN] fp32
+  int* tick;             // [8 * tiles] int32, zero between launches (per device and stream)
+  float* ws;             // [tiles * (S - 1) * 256 * BN] fp32
 };
 
 // (tm, tn) of workgroup bid (returned by value: through references the pair went to scratch)
@@ -406,14 +406,18 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(W4Args p) {
   const int wm = wid >> 1, wn = wid & 1;
   constexpr int BN = 32 * NJ, NW = 16 * NJ;
   const int ntiles = p.tiles_m * p.tiles_n;
-  const int ks = blockIdx.x / ntiles;        // K half of a split-K tile (0 without split)
+  const int nsplit = p.splits > 1 ? p.splits : 1;
+  const int ks = blockIdx.x / ntiles;        // K slice of a split-K tile (0 without split)
   const int tb = blockIdx.x - ks * ntiles;   // output tile
   const int2 tt = tile_of(tb, p.tiles_m, p.tiles_n, p.nfast);
   const int tm = tt.x, tn = tt.y;
   const int m0 = tm * BM, n0 = tn * BN;
   const int f0 = tn * NW;  // W4_SWIGLU: first feature of the tile (NW features of w1 and of w3)
-  const int nk = p.K / BK / (p.splits > 1 ? p.splits : 1);  // K-tiles of this workgroup (even)
-  const long k0 = (long)ks * nk * BK;        // its first k
+  // K-tiles in pairs; slice ks takes pairs [np * ks / S, np * (ks + 1) / S) (host: np >= S)
+  const int npairs = p.K / (2 * BK);
+  const int kp0 = npairs * ks / nsplit, kp1 = npairs * (ks + 1) / nsplit;
+  const int nk = 2 * (kp1 - kp0);            // K-tiles of this workgroup (even)
+  const long k0 = (long)kp0 * 2 * BK;        // its first k
 
   // LDS-DMA sources. Instruction q of wave w fills image piece P = q * 4 + w (bytes [P KiB, +1 KiB)),
   // lane L its 16 B at P KiB + 16 L; the lane's source is the element that image slot holds.
@@ -539,17 +543,20 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(W4Args p) {
 
   // (the dW layout, k-major A, has no split-K: its tile grids fill the chip, and the extra live
   // registers of the hand-off pushed its widest tile into scratch)
-  const float4* split_slot = nullptr;  // split-K second half: the first half's partial (uniform)
+  const float4* split_slot = nullptr;  // split-K consumer: slice 0's partial (uniform)
   if constexpr ((EPI == W4_STORE || EPI == W4_RES) && !AT) {
-    if (p.splits > 1) {  // uniform (2: host-checked)
+    if (nsplit > 1) {  // uniform (2 .. 8: host-checked)
       // Static roles, wave-uniform control flow (no single-lane branches near the 256 live
-      // accumulators: those made the compiler copy them to VGPRs and spill): the first half of K
-      // (ks 0, the lower block ids: dispatched first) parks its partial and raises the tile's flag;
-      // the second half (ks 1) waits for that flag. A waiting workgroup never holds back its
-      // producer: the producers are dispatched ahead of it and wait on nothing.
-      float4* slot = reinterpret_cast<float4*>(p.ws) + ((long)tb * 4 + wid) * (8 * NJ * 64) + lane;
-      int* flag = p.tick + tb;
-      if (ks == 0) {
+      // accumulators: those made the compiler copy them to VGPRs and spill): slices 0 .. S-2 (the
+      // lower block ids: dispatched first) park their partials and raise their flags; the last
+      // slice waits for all of them and adds them in slice order in its epilogue (fixed order:
+      // deterministic). A waiting workgroup never holds back a producer: the producers are
+      // dispatched ahead of it and wait on nothing.
+      constexpr long SLOT = 4L * 8 * NJ * 64;  // float4 per partial tile
+      float4* slot = reinterpret_cast<float4*>(p.ws) + ((long)tb * (nsplit - 1) + ks) * SLOT +
+                     (long)wid * (8 * NJ * 64) + lane;
+      int* flags = p.tick + (long)tb * 8;
+      if (ks < nsplit - 1) {
         // stored straight from the AGPRs (asm "a" operands, no VGPR copies of the accumulators);
         // 1 KiB per wave store, 4 stores per 4 KiB window of the base (13-bit signed immediate)
 #pragma unroll
@@ -565,23 +572,26 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(W4Args p) {
         if (wid == 0) {  // the whole wave (one address, one value)
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          __hip_atomic_store(flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(flags + ks, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         return;
       }
       if (wid == 0) {
-        // bounded (2^22 polls, a few seconds) so a broken hand-off cannot hang the GPU
+        // lane l watches slice (l & 7)'s flag; bounded (2^22 polls, a few seconds) so a broken
+        // hand-off cannot hang the GPU
+        int* fl = flags + (lane & 7);
+        const bool watch = (lane & 7) < nsplit - 1;
         for (int n = 0; n < (1 << 22); ++n) {
-          const int v = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if (__builtin_amdgcn_readfirstlane(v) != 0) break;
+          const int v = __hip_atomic_load(fl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (__all(!watch || v != 0)) break;
           __builtin_amdgcn_s_sleep(4);
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        __hip_atomic_store(flag, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-armed
+        __hip_atomic_store(fl, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-armed (all 8)
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
-      split_slot = slot;  // the epilogue adds the first half's partial as it converts (below)
+      split_slot = slot - (long)ks * SLOT;  // slice 0's partial; the epilogue adds them as it converts
     }
   }
 
@@ -593,27 +603,39 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(W4Args p) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int m = i * 16 + lr;
-      // split-K: + the first half's fp32 partial, element by element (fragment order, one row of
-      // fragments at a time: the sums are consumed here, never all live at once)
-      float4 o[NJ];
+      // split-K: the partials of slices 0 .. S-2 summed in slice order, then + this slice's own
+      // accumulators (fragment order, one row of fragments at a time: the sums are consumed
+      // here, never all live at once)
+      float4 ps[NJ];
       if (split_slot != nullptr) {
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) o[j] = split_slot[(i * NJ + j) * 64];
+        for (int j = 0; j < NJ; ++j) ps[j] = split_slot[(i * NJ + j) * 64];
+        for (int sl = 1; sl < nsplit - 1; ++sl) {
+          const float4* q = split_slot + (long)sl * (4L * 8 * NJ * 64);
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) {
+            const float4 t = q[(i * NJ + j) * 64];
+            ps[j].x += t.x;
+            ps[j].y += t.y;
+            ps[j].z += t.z;
+            ps[j].w += t.w;
+          }
+        }
       }
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
         const int ch = 2 * j + (hc >> 1);
         f32x4_t v = acc[i][j];
         if (split_slot != nullptr) {
-          v[0] += o[j].x;
-          v[1] += o[j].y;
-          v[2] += o[j].z;
-          v[3] += o[j].w;
+          v[0] = ps[j].x + v[0];
+          v[1] = ps[j].y + v[1];
+          v[2] = ps[j].z + v[2];
+          v[3] = ps[j].w + v[3];
         }
-        uint2 o;
-        o.x = pk2<E>(v[0], v[1]);
-        o.y = pk2<E>(v[2], v[3]);
-        *reinterpret_cast<uint2*>(wl + m * 256 + ((ch ^ (m & 15)) << 4) + (hc & 1) * 8) = o;
+        uint2 pk;
+        pk.x = pk2<E>(v[0], v[1]);
+        pk.y = pk2<E>(v[2], v[3]);
+        *reinterpret_cast<uint2*>(wl + m * 256 + ((ch ^ (m & 15)) << 4) + (hc & 1) * 8) = pk;
       }
     }
   }

@@ -46,9 +46,9 @@ int pick_nj(long M, long N, bool kmajor_a = false) {
 }
 
 // Split-K (gemm_w4.h, W4Args::splits): a tile grid that fills under half the chip runs each tile
-// as two workgroups over the halves of K, when both halves keep >= 16 K-tiles (the 8B dX products
-// with N_out = 4096: qkv K = 6144, wo 4096, w13 28672, head 131072 at M = 2048: 128 tiles of 256
-// columns -> 256 workgroups). FT_W4_SPLITK=0 disables it (A/B), =2 forces it where it fits.
+// as S = 2 / 4 / 8 workgroups over slices of K of >= 16 K-tiles each (the 8B dX products with N_out
+// = 4096 at M = 2048: 128 tiles of 256 columns x 2; the GPT-2 LM-head dX, N_out = 768 / 1024, K =
+// V: 24 / 32 tiles x 8). FT_W4_SPLITK=0 disables it (A/B), =2 forces a split of 2 where it fits.
 int g_splitk_mode = [] {
   const char* e = std::getenv("FT_W4_SPLITK");
   return e == nullptr ? 1 : std::atoi(e);
@@ -65,41 +65,56 @@ Plan pick_plan(long M, long N, long K, bool kmajor_a, bool kmajor_b) {
   const long tm = M / BM, nkt = K / BK;
   Plan best{pick_nj(M, N, kmajor_a), 1};
   if (g_splitk_mode == 0 || best.nj == 0 || kmajor_a) return best;
+  // per slice: its K-tiles, the epilogue (~3 K-tiles), the partial's store (~3) and, for the last
+  // slice, reading the S - 1 partials (~3 each)
   auto cost = [&](int nj, int sp) {
     const long tiles = tm * (N / (32L * nj));
     const long rounds = (tiles * sp + 255) / 256;
     const double eff = nj == 8 ? 1.0 : nj == 7 ? 0.99 : nj == 6 ? 0.98 : (kmajor_a ? 0.65 : kmajor_b ? 0.85 : 0.92);
-    return (double)rounds * nj * ((double)nkt / sp + 3.0 + (sp > 1 ? 6.0 : 0.0)) / eff;
+    return (double)rounds * nj * ((double)nkt / sp + 3.0 + (sp > 1 ? 3.0 * sp : 0.0)) / eff;
   };
   double bc = cost(best.nj, 1);
   for (int nj : {8, 7, 6, 4}) {
-    if (N % (32L * nj) || K % (2 * BK * 2) || nkt / 2 < 16) continue;
+    if (N % (32L * nj)) continue;
     const long tiles = tm * (N / (32L * nj));
-    if (tiles * 2 > 256 && g_splitk_mode != 2) continue;  // the tiles alone fill the chip
-    const double c = cost(nj, 2);
-    if (c < bc - 1e-9 || g_splitk_mode == 2) {
-      bc = c;
-      best = Plan{nj, 2};
-      if (g_splitk_mode == 2) break;
+    for (int sp : {2, 4, 8}) {
+      if (nkt / sp < 16 || (K / (2 * BK)) < sp) continue;
+      if (tiles * sp > 256) continue;  // one round: every slice co-resident with its tile's others
+      if (g_splitk_mode == 2 && sp != 2) continue;
+      const double c = cost(nj, sp);
+      if (c < bc - 1e-9 || (g_splitk_mode == 2 && best.splits == 1)) {
+        bc = c;
+        best = Plan{nj, sp};
+      }
     }
   }
   return best;
 }
 
 // Split-K hand-off flags: one zeroed int32 buffer per (device, stream), grown on demand and kept
-// (each tile's second half re-arms its flag, so the buffer is zero between launches; launches on
-// one stream are ordered, two streams never share flags). Under stream capture a buffer that
-// would have to be (re)allocated is not: the caller runs without split (nullptr).
+// (each tile's last slice re-arms its flags, so the buffer is zero between launches; launches on
+// one stream are ordered, two streams never share flags). Under stream capture nothing is
+// allocated: the capture stream borrows the device's first buffer (a captured graph replays on
+// the stream that ran the eager steps before it, so the two never run at once), else the caller
+// runs without split (nullptr) -- and a graph then sums in another order than the eager step.
 int* splitk_ticks(const c10::Device& dev, hipStream_t st, long n) {
   static std::mutex mu;
   static std::map<std::pair<int, hipStream_t>, at::Tensor> bufs;
+  static std::map<int, at::Tensor> first;
   std::lock_guard<std::mutex> lock(mu);
-  at::Tensor& b = bufs[{dev.index(), st}];
-  if (!b.defined() || b.numel() < n) {
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
-    b = at::zeros({std::max(n, 8192L)}, at::TensorOptions().device(dev).dtype(at::kInt));
+  auto it = bufs.find({dev.index(), st});
+  if (it != bufs.end() && it->second.numel() >= n) return it->second.data_ptr<int>();
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) {
+    auto f = first.find(dev.index());
+    return (f != first.end() && f->second.numel() >= n) ? f->second.data_ptr<int>() : nullptr;
   }
+  static std::vector<at::Tensor> keep;  // never freed: a captured graph may hold a replaced one
+  at::Tensor b = at::zeros({std::max(n, 65536L)}, at::TensorOptions().device(dev).dtype(at::kInt));
+  keep.push_back(b);
+  bufs[{dev.index(), st}] = b;
+  auto f = first.find(dev.index());
+  if (f == first.end() || f->second.numel() < b.numel()) first[dev.index()] = b;
   return b.data_ptr<int>();
 }
 
@@ -109,14 +124,14 @@ int* splitk_ticks(const c10::Device& dev, hipStream_t st, long n) {
 void setup_split(W4Args& p, int splits, int nj, const at::Tensor& like, at::Tensor& ws_hold) {
   p.splits = 1;
   if (splits < 2) return;
-  TORCH_CHECK(splits == 2, "gemm_w4: split-K of 2 only");
-  TORCH_CHECK(p.K % (2 * BK * 2) == 0, "gemm_w4: split-K needs K % 256");
+  TORCH_CHECK(splits <= 8, "gemm_w4: split-K of 2 .. 8");
+  TORCH_CHECK(p.K / (2 * BK) >= splits, "gemm_w4: split-K needs K / 128 >= splits");
   TORCH_CHECK(p.lda == p.K, "gemm_w4: split-K is built for K-contiguous A (forward / dX)");
   const long tiles = (long)p.tiles_m * p.tiles_n;
-  int* t = splitk_ticks(like.device(), ft_stream(), tiles);
+  int* t = splitk_ticks(like.device(), ft_stream(), 8 * tiles);
   if (t == nullptr) return;
-  ws_hold = at::empty({tiles * BM * 32L * nj}, like.options().dtype(at::kFloat));
-  p.splits = 2;
+  ws_hold = at::empty({tiles * (splits - 1) * BM * 32L * nj}, like.options().dtype(at::kFloat));
+  p.splits = splits;
   p.tick = t;
   p.ws = ws_hold.data_ptr<float>();
 }

@@ -50,7 +50,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--steps", type=int, default=8)
     ap.add_argument("--rounds", type=int, default=3)
-    ap.add_argument("--knobs", default="hand_dw,dw")
+    ap.add_argument("--knobs", default="splitk")
     a = ap.parse_args()
 
     from fault_tolerant_llm_training_amd.data.synthetic import SyntheticTokens
@@ -104,38 +104,15 @@ def main():
         torch.cuda.synchronize()
         torch.cuda.set_stream(hp if on else default_stream)
 
-    def hand(kind):
-        def set_(on):
-            torch.cuda.synchronize()
-            (Fx._HAND_AUTO.add if on else Fx._HAND_AUTO.discard)(kind)
-        return set_
-
-    def shapes(spec):
-        sh = Fx._parse_shapes(spec)
-
-        def set_(on):
-            torch.cuda.synchronize()
-            for x in sh:
-                (Fx._HAND_SHAPES.add if on else Fx._HAND_SHAPES.discard)(x)
-        return set_
-
-    setters = {"hand_dw": hand("dw"), "hand_dx": hand("dx"),
-               # Llama-3-8B dW of wo and w2 (the products where the hand kernel >= hipBLASLt alone)
-               "hand_dw_wo_w2": shapes("dw:4096x4096x2048,dw:4096x14336x2048"),
-               "hand_dw_wo": shapes("dw:4096x4096x2048"), "dw": Fx.set_dw_stream, "tonly": Fx.set_ffn_t_only,
-               "dkdv2": kernels().flash_set_dkdv2, "prio": set_prio, "sumsq_end": ddp_mod.set_sumsq_at_end,
-               "qkvrope": Fx.set_qkv_rope, "w4fwd": Fx.set_w4_fwd, "w4dw": Fx.set_w4_dw,
-               "notrans": lambda on: setattr(Fx, "_DW_MODE", "none" if on else "auto"),
+    setters = {"dw": Fx.set_dw_stream, "dkdv2": kernels().flash_set_dkdv2, "prio": set_prio,
+               "sumsq_end": ddp_mod.set_sumsq_at_end, "qkvrope": Fx.set_qkv_rope, "w4fwd": Fx.set_w4_fwd,
                "fastmath": lambda on: (torch.cuda.synchronize(), kernels().set_exact_math(not on)),
                "w4swiglu": lambda on: (torch.cuda.synchronize(), Fx.set_w4_swiglu(on)),
                "w4bwd": lambda on: (torch.cuda.synchronize(), Fx.set_w4_bwd(on)),
                "psums": lambda on: (torch.cuda.synchronize(), red.set_producer_sums(on)),
-               "w4head": lambda on: (torch.cuda.synchronize(), Fx.set_w4_head(on)),
                "splitk": lambda on: (torch.cuda.synchronize(), Fx.set_w4_splitk(1 if on else 0)),
                "w4dwside": lambda on: (torch.cuda.synchronize(), setattr(Fx, "_W4_DW_SIDE", on)),
-               "r4": lambda on: (torch.cuda.synchronize(), Fx.set_w4_bwd(on), red.set_producer_sums(on),
-                                 Fx.set_w4_head(on)),
-               "w4wide": lambda on: (torch.cuda.synchronize(), setattr(Fx, "_W4_FWD_MAX_NJ", 8 if on else 6))}
+               "gemm_s": lambda on: (torch.cuda.synchronize(), Fx.set_gemm_s(on))}
     configs = list(itertools.product([False, True], repeat=len(knobs)))
 
     def apply(cfg):

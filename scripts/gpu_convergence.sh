@@ -2,7 +2,7 @@
 # Does the MI355X kernel set learn like the plain path? Byte-level text (a generated parquet), the same
 # seed and data order, two runs per model: the default kernels (w4 forward GEMMs with the RoPE / SwiGLU
 # epilogues, hardware rcp/sqrt in AdamW and SwiGLU) vs hipBLASLt for every GEMM, the separate RoPE and
-# SwiGLU kernels and IEEE division/sqrt (FT_GEMM=blas FT_EXACT_MATH=1).
+# SwiGLU kernels and IEEE division/sqrt (FT_GEMM_BLAS=1 FT_EXACT_MATH=1).
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out/conv
 D=/tmp/convdata; mkdir -p $D
@@ -17,9 +17,9 @@ run() {  # run <name> <timeout> <env...> -- <args>
 L8="--learning-rate 1e-4 --lr-warmup-steps 50 --training-steps 400 --logging-frequency 10 --checkpoint-path /tmp/convck --save-every 0"
 G2="--model gpt2-medium --hip-graph --learning-rate 3e-4 --lr-warmup-steps 100 --training-steps 2000 --logging-frequency 25 --checkpoint-path /tmp/convck --save-every 0"
 run llama8b_default 240 FT_NONE=1 -- $L8
-run llama8b_plain 240 FT_GEMM=blas FT_EXACT_MATH=1 -- $L8
+run llama8b_plain 240 FT_GEMM_BLAS=1 FT_EXACT_MATH=1 -- $L8
 run gpt2m_default 240 FT_NONE=1 -- $G2
-run gpt2m_plain 240 FT_GEMM=blas FT_EXACT_MATH=1 -- $G2
+run gpt2m_plain 240 FT_GEMM_BLAS=1 FT_EXACT_MATH=1 -- $G2
 {
   echo "# Convergence on MI355X: default kernels vs the plain path (scripts/gpu_convergence.sh)"
   echo

@@ -59,9 +59,7 @@ case("norm_bwd 1-wave-per-row (A/B)", lambda: K.norm_bwd(dy, h, w, rstd, None, d
 os.environ.pop("FT_NORM_BWD_SPLIT")
 case("norm_bwd split-row (again)", lambda: K.norm_bwd(dy, h, w, rstd, None, dw, dres, False), 4 * T * D * 2)
 gu = r(T, 2 * F)
-case("swiglu_fwd_t (a + a^T) [2048x14336]", lambda: K.swiglu_fwd_t(gu), (2 * T * F + 2 * T * F) * 2)
 da = r(T, F)
-case("swiglu_bwd_t (dgu + dgu^T)", lambda: K.swiglu_bwd_t(da, gu), (T * F + 2 * T * F + 4 * T * F) * 2)
 qkv = r(T, (Hq + 2 * Hkv) * HD)
 cos, sin = rope_tables(HD, T, 500000.0)
 cos, sin = cos.cuda(), sin.cuda()
@@ -69,8 +67,6 @@ case("rope_fwd (q,k of packed qkv)", lambda: K.rope_fwd(qkv, cos, sin, T, Hq, Hk
      2 * T * (Hq + Hkv) * HD * 2)
 g2 = r(T, (Hq + 2 * Hkv) * HD)
 case("rope_bwd_ (in place)", lambda: K.rope_bwd_(g2, cos, sin, T, Hq, Hkv, HD), 2 * T * (Hq + Hkv) * HD * 2)
-xt = r(T, D)
-case("transpose2d [2048x4096]", lambda: K.transpose2d(xt), 2 * T * D * 2)
 logits = (3 * torch.randn(T, V, device="cuda")).bfloat16()
 lab = torch.randint(0, V, (T,), device="cuda")
 case("xent_fwd [2048x131072]", lambda: K.xent_fwd(logits, lab, -100), T * V * 2)

@@ -245,15 +245,19 @@ def test_activation_checkpointing_bitwise():
             assert torch.equal(x, y)
 
 
-@pytest.mark.parametrize("dw_mode", ["all", "none"])
-def test_dw_side_stream_bitwise(dw_mode, monkeypatch):
-    """Weight-gradient GEMMs on the side stream (concurrent with dX) give bit-identical training."""
+@pytest.mark.parametrize("w4", [False, True])
+def test_dw_side_stream_bitwise(w4, monkeypatch):
+    """Weight-gradient GEMMs on the side stream (concurrent with dX) give bit-identical training,
+    for the hipBLASLt dW (side stream) and the w4 dW (inline by default, forced onto the side
+    stream here)."""
     from fault_tolerant_llm_training_amd.models.llama import build_model, model_args_for
     from fault_tolerant_llm_training_amd.ops import functional as Fx
     from fault_tolerant_llm_training_amd.optim.adamw import FlatAdamW
     from fault_tolerant_llm_training_amd.parallel.ddp import GradReducer
 
-    monkeypatch.setattr(Fx, "_DW_MODE", dw_mode)
+    if w4:
+        monkeypatch.setattr(Fx, "_W4_MIN_TILES", 1)
+        monkeypatch.setattr(Fx, "_W4_DW_SIDE", True)
     a = model_args_for("tiny", vocab_size=1024, seq_len=256)
     tok = torch.randint(0, 1024, (2, 256), device="cuda")
     lab = torch.randint(0, 1024, (2, 256), device="cuda")
@@ -281,47 +285,16 @@ def test_dw_side_stream_bitwise(dw_mode, monkeypatch):
     assert torch.equal(g0, g1) and torch.equal(p0, p1) and torch.equal(l0, l1)
 
 
-@pytest.mark.parametrize("R,C", [(64, 64), (2048, 4096), (128, 28672), (4096, 192)])
-def test_transpose2d(K, R, C):
-    x = torch.randn(R, C, device="cuda").bfloat16()
-    assert torch.equal(K.transpose2d(x), x.t().contiguous())
-
-
-@pytest.mark.parametrize("mode", ["all", "none"])
-def test_weight_grad_layouts(mode, monkeypatch):
+def test_weight_grad_blas_route():
+    """A dW too small for the w4 kernel goes to hipBLASLt (dy^T x on the stored layouts) vs fp32."""
     from fault_tolerant_llm_training_amd.ops import functional as Fx
 
-    monkeypatch.setattr(Fx, "_DW_MODE", mode)
     dy = torch.randn(256, 384, device="cuda").bfloat16()
     x = torch.randn(256, 128, device="cuda").bfloat16()
+    assert not Fx._w4_dw_ok(256, 384, 128, dy, x)
     dw = Fx.weight_grad(dy, x, None)
     ref = dy.float().t() @ x.float()
     assert rel(dw, ref) < 1e-2
-
-
-@pytest.mark.parametrize("given_t", [False, True])
-def test_weight_grad_hand_shapes(given_t, monkeypatch):
-    """A product listed in _HAND_SHAPES runs on the hand GEMM (asm-read dW kernel), from the
-    row-major X or from X^T (the SwiGLU kernels' a^T), into a sink with accumulation."""
-    from fault_tolerant_llm_training_amd.ops import functional as Fx
-    from fault_tolerant_llm_training_amd.ops.grad_sink import GradSink
-
-    T, N, Kd = 512, 256, 768
-    monkeypatch.setattr(Fx, "_HAND_SHAPES", {("dw", N, Kd, T)})
-    dy = torch.randn(T, N, device="cuda").bfloat16()
-    x = torch.randn(T, Kd, device="cuda").bfloat16()
-    ref = dy.float().t() @ x.float()
-    dw = Fx.weight_grad(dy, None, None, xT=x.t().contiguous()) if given_t else Fx.weight_grad(dy, x, None)
-    assert rel(dw, ref) < 1e-2
-    buf = torch.randn(N * Kd, device="cuda").bfloat16()
-    base = buf.float().clone()
-    sink = GradSink(buf)
-    sink.accumulate = True
-    if given_t:
-        Fx.weight_grad(dy, None, sink, xT=x.t().contiguous())
-    else:
-        Fx.weight_grad(dy, x, sink)
-    assert rel(buf.view(N, Kd), base.view(N, Kd) + ref) < 1e-2
 
 
 @pytest.mark.parametrize("ln", [False, True])
@@ -360,35 +333,22 @@ def test_pinned_ring_h2d():
     release()
 
 
-@pytest.mark.parametrize("T,F_", [(64, 64), (192, 320), (512, 1408), (256, 14336)])
-def test_swiglu_transposed_outputs(K, T, F_):
-    """Tiled SwiGLU kernels: the row-major outputs equal the elementwise kernels' bitwise,
-    and the extra transposed outputs are exact transposes (plain=False writes only the
-    transpose)."""
-    gu = torch.randn(T, 2 * F_, device="cuda").bfloat16()
-    a, aT = K.swiglu_fwd_t(gu)
-    assert torch.equal(a, K.swiglu_fwd(gu)) and torch.equal(aT, a.t().contiguous())
-    da = torch.randn(T, F_, device="cuda").bfloat16()
-    dgu, dguT = K.swiglu_bwd_t(da, gu)
-    empty, dguT2 = K.swiglu_bwd_t(da, gu, False)
-    assert torch.equal(dgu, K.swiglu_bwd(da, gu)) and torch.equal(dguT, dgu.t().contiguous())
-    assert empty.numel() == 0 and torch.equal(dguT2, dguT)
-
-
-@pytest.mark.parametrize("mode,t_only", [("all", False), ("all", True), ("none", False)])
-def test_feed_forward_fused(mode, t_only, monkeypatch):
-    """FeedForwardFn (GEMM → tiled SwiGLU with transposed outputs → GEMM, weight grads into
-    sinks) vs fp32 autograd of w2(silu(x w1^T) * (x w3^T))."""
+@pytest.mark.parametrize("w4", [False, True])
+def test_feed_forward_fused(w4, monkeypatch):
+    """The FFN node (GEMM -> SwiGLU -> GEMM, or every product on the w4 kernel with the SwiGLU
+    epilogues: FeedForwardW4Fn), weight grads into sinks, vs fp32 autograd of
+    w2(silu(x w1^T) * (x w3^T)) (reference model.py:254)."""
     from fault_tolerant_llm_training_amd.ops import functional as Fx
     from fault_tolerant_llm_training_amd.ops.grad_sink import GradSink
 
-    monkeypatch.setattr(Fx, "_DW_MODE", mode)
-    monkeypatch.setattr(Fx, "_FFN_T_ONLY", t_only)
+    if w4:
+        monkeypatch.setattr(Fx, "_W4_MIN_TILES", 1)
     torch.manual_seed(5)
-    T, D, Fh = 256, 192, 320
+    T, D, Fh = 256, 256, 896  # F % 112 (SwiGLU tile), 2F % 256 (dW13 rows)
     x = torch.randn(T, D, device="cuda").bfloat16().requires_grad_(True)
     w13 = (0.05 * torch.randn(2 * Fh, D, device="cuda")).bfloat16()
     w2 = (0.05 * torch.randn(D, Fh, device="cuda")).bfloat16()
+    assert Fx._ffn_w4t_ok(x.detach(), w13, w2) == w4
     g13 = torch.empty(w13.numel(), dtype=torch.bfloat16, device="cuda")
     g2 = torch.empty(w2.numel(), dtype=torch.bfloat16, device="cuda")
     y = Fx.feed_forward(x, w13, w2, GradSink(g13), GradSink(g2))

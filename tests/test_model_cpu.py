@@ -131,11 +131,11 @@ def test_activation_checkpointing_same_loss_and_grads(n, recompute_attention):
 def test_selective_checkpointing_skips_attention_recompute(monkeypatch):
     """Kept attention outputs: the backward recompute runs no attention forward, a forward whose
     backward never ran leaves nothing stale, and gradients match the no-recompute model."""
-    from fault_tolerant_llm_training_amd.ops import functional as Fx
+    from fault_tolerant_llm_training_amd.ops import attention as A
 
     calls = []
-    real = Fx.attention_reference
-    monkeypatch.setattr(Fx, "attention_reference", lambda *x: calls.append(1) or real(*x))
+    real = A.attention_reference
+    monkeypatch.setattr(A, "attention_reference", lambda *x: calls.append(1) or real(*x))
     a = model_args_for("tiny", vocab_size=128, seq_len=32)
     tok = torch.randint(0, 128, (2, 32))
     lab = torch.randint(0, 128, (2, 32))

@@ -28,7 +28,9 @@ def gates(monkeypatch):
     from fault_tolerant_llm_training_amd.ops import functional as Fx
 
     monkeypatch.setattr(Fx, "_W4_MIN_TILES", 1)
-    monkeypatch.setattr(Fx, "_QKV_ROPE_MIN_K", 0)
+    from fault_tolerant_llm_training_amd.ops import attention as A
+
+    monkeypatch.setattr(A, "_QKV_ROPE_MIN_K", 0)
     return Fx
 
 
