@@ -148,10 +148,6 @@ def main():
     # raise (and report the error in the JSON line) instead of blocking for the 30-minute default
     info = fdist.init_distributed(a.device, timeout_s=300)
     dev = info.device
-    if os.environ.get("FT_COMPUTE_PRIORITY") == "1" and dev.type == "cuda":
-        # compute on a high-priority stream: its workgroups are dispatched ahead of the
-        # optimizer/snapshot side streams when both have work queued
-        torch.cuda.set_stream(torch.cuda.Stream(device=dev, priority=-1))
     world = info.world_size
     # what the job really runs on: process-group size (must be --gpus), one distinct GPU per rank
     # (raises otherwise), peer access between every pair, RCCL version -- recorded in the JSON line

@@ -999,7 +999,7 @@ struct GqaFold {
   bf16_t* dqkv;            // [T, (Hq + 2 Hkv) D]
   const float* cos_t;      // RoPE tables or null
   const float* sin_t;
-  int dbg;                 // timing experiments only (FT_FLASH_FOLD_DBG): 1 no fold work, 2 no release fence
+  int dbg;                 // timing experiments only: 1 no fold work, 2 no release fence
   int q_done;              // dQ already rotated by the dQ kernel
 };
 
@@ -1799,8 +1799,7 @@ at::Tensor flash_bwd(const at::Tensor& dout, const at::Tensor& qk, const at::Ten
   const long rows = (long)T * Hq;
   // GQA fold inside the deterministic dK/dV kernel (no finalize launch): its tile counters
   static const int fold_dbg = [] {
-    const char* e = std::getenv("FT_FLASH_FOLD_DBG");
-    return e == nullptr ? 0 : std::atoi(e);
+    return 0;  // (1: no fold work, 2: no release fence -- the timing experiments of r4_flash_gqa_fold_probe)
   }();
   // RoPE backward of dQ in the dQ kernel's epilogue (deterministic mode, GQA partials to fold; the
   // direct no-GQA path rotates Q and K in one rope_bwd_ pass)

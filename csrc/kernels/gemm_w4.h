@@ -202,6 +202,7 @@ struct W4Args {
   // wave store) and raise flag tick[8 tile + slice]; the last slice adds them in slice order to
   // its own in the epilogue (fixed order: deterministic) and re-arms the flags for the next launch.
   int splits;
+  int dbg;               // timing probes only (gemm_w4_set_dbg): bit 0 = skip the epilogue's global stores
   int* tick;             // [8 * tiles] int32, zero between launches (per device and stream)
   float* ws;             // [tiles * (S - 1) * 256 * BN] fp32
 };
@@ -719,7 +720,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(W4Args p) {
 #pragma unroll
         for (int q = 0; q < 8; ++q) sq = fmaf(a[q], a[q], sq);
       }
-      *reinterpret_cast<uint4*>(p.c + gm * p.ldc + gn) = v;
+      if (!(p.dbg & 1)) *reinterpret_cast<uint4*>(p.c + gm * p.ldc + gn) = v;
     }
   }
   if (p.part != nullptr) {  // uniform: one partial per tile, fixed order (deterministic)

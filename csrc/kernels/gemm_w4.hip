@@ -121,7 +121,10 @@ int* splitk_ticks(const c10::Device& dev, hipStream_t st, long n) {
 // Sets p.splits (1 or 2) and the split's hand-off words / fp32 workspace; `ws_hold` keeps the
 // workspace alive until the launch is enqueued (the caching allocator orders its reuse on the
 // stream). Falls back to one workgroup per tile where the split cannot run.
+int g_dbg = 0;  // timing probes (gemm_w4_set_dbg): W4Args::dbg of every launch
+
 void setup_split(W4Args& p, int splits, int nj, const at::Tensor& like, at::Tensor& ws_hold) {
+  p.dbg = g_dbg;
   p.splits = 1;
   if (splits < 2) return;
   TORCH_CHECK(splits <= 8, "gemm_w4: split-K of 2 .. 8");
@@ -392,6 +395,10 @@ int64_t gemm_w4_pick(int64_t M, int64_t N) { return pick_nj(M, N); }
 // FT_W4_SPLITK at run time (A/B): 0 off, 1 automatic, 2 forced where it fits
 void gemm_w4_set_splitk(int64_t mode) { g_splitk_mode = (int)mode; }
 
+// timing probes only (scripts/w4_overhead_probe.py): bit 0 skips the store / residual epilogues'
+// global stores (the output is left unwritten)
+void gemm_w4_set_dbg(int64_t v) { g_dbg = (int)v; }
+
 // (tile width / 32, splits) the automatic choice takes for C[M, N] over a K-deep sum
 std::vector<int64_t> gemm_w4_plan(int64_t M, int64_t N, int64_t K, bool a_t, bool b_t) {
   const Plan pl = pick_plan(M, N, K, a_t, b_t);
@@ -407,6 +414,7 @@ TORCH_LIBRARY_FRAGMENT(ftamd, m) {
       &gemm_w4_ex);
   m.def("gemm_w4_plan(int M, int N, int K, bool a_t=False, bool b_t=False) -> int[]", &gemm_w4_plan);
   m.def("gemm_w4_set_splitk(int mode) -> ()", &gemm_w4_set_splitk);
+  m.def("gemm_w4_set_dbg(int v) -> ()", &gemm_w4_set_dbg);
   m.def("gemm_qkv_rope_w4(Tensor x, Tensor w, Tensor cos, Tensor sin, int seq, int hq, int hkv, int d) -> Tensor",
         &gemm_qkv_rope_w4);
   m.def("gemm_w4_pick(int M, int N) -> int", &gemm_w4_pick);

@@ -62,14 +62,9 @@ struct V8 {
   }
 };
 
-// FT_STREAM_NT=0 selects plain loads/stores for the optimizer-pass kernels (A/B).
-bool stream_nt() {
-  static const bool nt = [] {
-    const char* e = std::getenv("FT_STREAM_NT");
-    return e == nullptr || std::atoi(e) != 0;
-  }();
-  return nt;
-}
+// Non-temporal loads/stores for the optimizer-pass kernels (plain ones measured slower:
+// profiles/r1_stream_nt_ab.log).
+bool stream_nt() { return true; }
 
 constexpr int NORM_BLOCKS = 2048;
 

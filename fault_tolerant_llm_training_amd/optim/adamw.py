@@ -35,7 +35,6 @@ leaves behind (reference utils.py:61, train.py:107-109).
 from __future__ import annotations
 
 import math
-import os
 from typing import List, Optional, Tuple
 
 import torch
@@ -124,7 +123,7 @@ class FlatAdamW(torch.optim.Optimizer):
         self._hyper_i = 0
         # grid cap for the per-bucket AdamW launches that run concurrently with the next
         # forward's GEMMs (fewer blocks = less contention for CU issue slots)
-        self.overlap_blocks = int(os.environ.get("FT_ADAMW_BLOCKS", "0"))
+        self.overlap_blocks = 0  # grid cap of the pipelined per-bucket launches (A/B: r2_adamw_overlap_cap.log)
         # parameter index (reference order) -> flat slot
         name_of = {id(p): n for n, p in flat.param_objs.items()}
         self._index_slots = [flat.slots[name_of[id(p)]] for p in params]

@@ -65,7 +65,7 @@ MODES = ("local", "allreduce", "zero1")
 PARTIALS_PER_BUCKET = 512
 # A/B switch (scripts/ab_step.py): take every bucket's sum of squares in one pass after
 # backward instead of as each bucket completes (the default overlaps them with backward)
-SUMSQ_AT_END = os.environ.get("FT_SUMSQ_AT_END", "0") == "1"
+SUMSQ_AT_END = False
 
 
 def set_sumsq_at_end(on: bool) -> None:
@@ -77,9 +77,9 @@ def set_sumsq_at_end(on: bool) -> None:
 # write the gradients (the w4 dW GEMM's epilogue per output tile, the norm backward's column sums
 # per 32 columns) into a per-sink slice of ``partials``; only gradients whose producer has no such
 # epilogue (the embedding's scatter-add, hipBLASLt fallbacks) get the separate sumsq pass. The
-# 16 GB re-read of the Llama-3-8B gradient per step is gone. FT_FUSED_SUMSQ=0: per-bucket passes.
+# 16 GB re-read of the Llama-3-8B gradient per step is gone. set_fused_sumsq(False): per-bucket passes.
 # (Under DP the norm is of the REDUCED gradient, so the passes run after each bucket's collective.)
-FUSED_SUMSQ = os.environ.get("FT_FUSED_SUMSQ", "1") == "1"
+FUSED_SUMSQ = True
 
 
 def set_fused_sumsq(on: bool) -> None:

@@ -51,6 +51,7 @@ def _step(m, tok, lab):
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
 def test_w4_paths_vs_cpu_and_blas(gates, dt):
     from fault_tolerant_llm_training_amd.models.llama import build_model
+    from fault_tolerant_llm_training_amd.ops import attention as A
 
     Fx = gates
     a = _args()
@@ -65,7 +66,7 @@ def test_w4_paths_vs_cpu_and_blas(gates, dt):
     w13 = mg.layers["0"].feed_forward.w13
     w2 = mg.layers["0"].feed_forward.w2.weight
     assert Fx._ffn_w4t_ok(x2, w13, w2)  # the FFN really takes FeedForwardW4Fn
-    assert Fx._qkv_rope_ok(x2, mg.layers["0"].attention.wqkv, a.head_dim)
+    assert A._qkv_rope_ok(x2, mg.layers["0"].attention.wqkv, a.head_dim)
     lg = _step(mg, tok.cuda(), lab.cuda())
     g_w4 = mg.flat.grads.clone()
     lc = _step(mc, tok, lab)
@@ -191,8 +192,9 @@ def test_fused_sumsq_fallback_then_producer(gates):
         red.set_producer_sums(producers)
         tok = torch.randint(0, a.vocab_size, (1, a.seq_len), device="cuda")
         red.begin_micro(0, 1)
-        # a loss scale that changes per step, so a stale partial cannot match by accident
-        (m(tok, tok) * (1.0 + 3 * it)).backward()
+        # a loss scale that changes per step, so a stale partial cannot match by accident (powers
+        # of two: the fused head's partials are of its unscaled dW times g^2, exact only then)
+        (m(tok, tok) * float(4 ** it)).backward()
         red.finish()
         torch.cuda.synchronize()
         want = m.flat.grads.double().pow(2).sum().item()
