@@ -1601,57 +1601,35 @@ __global__ __launch_bounds__(256) void flash_bwd_finalize_kernel(
   }
 }
 
-// Forward key split (see flash_fwd_kernel): -1 auto, 0 off, 1 on (FT_FLASH_FWD_SPLIT /
-// flash_set_fwd_split, for A/B).
-int g_fwd_split = [] {
-  const char* e = std::getenv("FT_FLASH_FWD_SPLIT");
-  return e == nullptr ? -1 : std::atoi(e);
-}();
+// Forward key split (see flash_fwd_kernel): -1 auto, 0 off, 1 on (flash_set_fwd_split, for A/B;
+// tests/test_flash_attn_gpu.py).
+int g_fwd_split = -1;
 
 // Software-pipelined forward (flash_fwd_pipe_kernel) for the unsplit grids: >= 1 on, 0 off
-// (FT_FLASH_FWD_PIPE / flash_set_fwd_pipe, for A/B). (A balanced variant — one 8-wave block per
-// query-tile pair, the long tile's keys split between the halves and merged in LDS — ran slower:
-// 60.0 vs 53.3 us at S = 2048, profiles/r3_flash_fwd_pipe.log.)
-int g_fwd_pipe = [] {
-  const char* e = std::getenv("FT_FLASH_FWD_PIPE");
-  return e == nullptr ? 1 : std::atoi(e);
-}();
+// (flash_set_fwd_pipe, for A/B). (A balanced variant — one 8-wave block per query-tile pair, the
+// long tile's keys split between the halves and merged in LDS — ran slower: 60.0 vs 53.3 us at
+// S = 2048, profiles/r3_flash_fwd_pipe.log.)
+int g_fwd_pipe = 1;
 
-// dQ key split (see flash_bwd_dq_kernel): -1 default (on), 0 off, 1 on (FT_FLASH_DQ_SPLIT /
-// flash_set_dq_split, for A/B).
-int g_dq_split = [] {
-  const char* e = std::getenv("FT_FLASH_DQ_SPLIT");
-  return e == nullptr ? -1 : std::atoi(e);
-}();
+// dQ key split (see flash_bwd_dq_kernel): -1 default (on), 0 off, 1 on (flash_set_dq_split, for A/B).
+int g_dq_split = -1;
 
-// dK/dV split of the slice-pair kernel: -1 auto, 0 off, 1 on (FT_FLASH_KV_SPLIT /
-// flash_set_kv_split, for A/B).
-int g_kv_split = [] {
-  const char* e = std::getenv("FT_FLASH_KV_SPLIT");
-  return e == nullptr ? -1 : std::atoi(e);
-}();
+// dK/dV split of the slice-pair kernel: -1 auto, 0 off, 1 on (flash_set_kv_split, for A/B).
+int g_kv_split = -1;
 
 // Deterministic backward, dK/dV stage: the slice-pair kernel (default) or the one-slice
-// flash_bwd_kernel<D, 1> (FT_FLASH_DKDV2=0 / flash_set_dkdv2, for A/B).
-bool g_dkdv2 = [] {
-  const char* e = std::getenv("FT_FLASH_DKDV2");
-  return e == nullptr || std::atoi(e) != 0;
-}();
-bool g_dkdv2_64 = [] {
-  const char* e = std::getenv("FT_FLASH_DKDV2");
-  return e != nullptr && std::atoi(e) == 2;
-}();
+// flash_bwd_kernel<D, 1> (flash_set_dkdv2, for A/B); the slice-pair kernel also for head_dim 64:
+// g_dkdv2_64 (measured slower there, off).
+bool g_dkdv2 = true;
+bool g_dkdv2_64 = false;
 
 // GQA fold of the deterministic backward in the separate finalize pass (default) or inside the
-// dK/dV kernel by each key tile's last q-head block (FT_FLASH_BWD_FOLD=1 / flash_set_bwd_fold).
+// dK/dV kernel by each key tile's last q-head block (flash_set_bwd_fold).
 // The in-kernel fold saves the launch but measured slower at the 8B layer (S = 2048, 32/8 heads,
 // RoPE): 296-307 us vs 175-193 us for the whole backward; its device-scope release fences and
 // counters alone cost ~16 us over the finalize variant without any fold work, and the folds run
 // as a 128-block tail behind the heaviest key tiles (profiles/r4_flash_gqa_fold_probe.log).
-bool g_bwd_fold = [] {
-  const char* e = std::getenv("FT_FLASH_BWD_FOLD");
-  return e != nullptr && std::atoi(e) != 0;
-}();
+bool g_bwd_fold = false;
 
 // The fold's per-tile arrival counters: one zeroed int32 buffer per device, grown on demand and
 // kept (each tile's last block re-arms its counter, so the buffer is zero between launches). One
@@ -1676,11 +1654,8 @@ int* fold_counters(const c10::Device& dev, long n) {
 // 12 / 16 heads x 16 tiles = 192 / 256 blocks at S = 2048), else 4.
 // The forward keeps 4-wave blocks (2 waves: 32.0 -> 36.6 us on GPT-2-small's layer); the
 // backward's dK/dV + dQ kernels gain (112.8 -> 94.2 us; 118.2 -> 99.2 us at 16 heads),
-// profiles/r2_flash_small_heads.log. FT_FLASH_NW=4 forces 4 (A/B).
-static const bool g_force_nw4 = [] {
-  const char* e = std::getenv("FT_FLASH_NW");
-  return e != nullptr && std::string(e) == "4";
-}();
+// profiles/r2_flash_small_heads.log.
+static const bool g_force_nw4 = false;
 int waves_per_block(long S, long B, long Hq, long D) {
   if (g_force_nw4) return 4;
   return (D == 64 && ((S + 127) / 128) * B * Hq < 512) ? 2 : 4;

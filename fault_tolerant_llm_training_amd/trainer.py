@@ -362,8 +362,7 @@ def train(args) -> int:
             os.unlink(ckpt_path + ".solo")
         except FileNotFoundError:
             pass
-    # FT_SHARDED_CKPT=1 forces the multi-writer protocol on a 1-rank process group (test hook)
-    sharded = info.world_size > 1 or (info.ckpt_group is not None and os.environ.get("FT_SHARDED_CKPT") == "1")
+    sharded = info.world_size > 1
 
     def ckpt_engine():
         if ckpt["engine"] is None:

@@ -253,7 +253,7 @@ def test_flash_bwd_with_rope_backward(B, S, Hq, Hkv, D, mode):
                                                (1, 1000, 4, 1, 128, True), (2, 512, 8, 2, 64, True),
                                                (1, 100, 6, 2, 64, False), (1, 512, 16, 1, 128, True)])
 def test_flash_bwd_in_kernel_gqa_fold(B, S, Hq, Hkv, D, rope):
-    """Deterministic backward, opt-in variant (FT_FLASH_BWD_FOLD=1): the GQA fold (+ RoPE backward)
+    """Deterministic backward, opt-in variant (flash_set_bwd_fold): the GQA fold (+ RoPE backward)
     done by the last q-head block of each key tile inside the dK/dV kernel == the finalize pass, bit
     for bit (same head order), and stays so over repeated launches (the counters re-arm)."""
     from fault_tolerant_llm_training_amd._native import kernels
