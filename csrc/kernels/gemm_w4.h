@@ -203,10 +203,6 @@ struct W4Args {
   // its own in the epilogue (fixed order: deterministic) and re-arms the flags for the next launch.
   int splits;
   int dbg;               // timing probes only (gemm_w4_set_dbg): bit 0 = skip the epilogue's global stores
-  // persistent grid (W4_STORE / W4_RES, no split): gridDim.x (a multiple of 8) workgroups walk the
-  // tiles bid, bid + grid, ...; the last two K-tiles of a tile already stage the next tile's first
-  // two (no pipeline refill between tiles), its epilogue runs through a separate 32 KiB of LDS
-  int persist;           // 0: one workgroup per tile (x splits); else the persistent grid size
   int* tick;             // [8 * tiles] int32, zero between launches (per device and stream)
   float* ws;             // [tiles * (S - 1) * 256 * BN] fp32
 };
@@ -290,8 +286,6 @@ struct Sched {
 
 struct Ctx {
   i32x4_t srdA, srdB;
-  i32x4_t srdA_n, srdB_n;           // the next tile's sources (persistent grid)
-  int has_next;                     // uniform: the last two K-tiles stage the next tile's first two
   unsigned voA[8], voB[8];
   unsigned rdA0, rdA1, rdB0, rdB1;  // K-contiguous images: k-step 0 / 1 lane address
   unsigned aT[8], bT[8];            // k-major images: lane address of fragment i (k-step 0, lo)
@@ -349,13 +343,8 @@ __device__ __forceinline__ void rd_slot(Frag<AT> (&ax)[8], Frag<BT> (&bx)[NJ], c
 template <class E, int NJ, bool AT, bool BT, int CUR, bool DMA, bool NEXT>
 __device__ __forceinline__ void ktile(f32x4_t (&acc)[8][NJ], Frags<NJ, AT, BT>& f, int t, int nk, const Ctx& c) {
   using S = Sched<NJ, AT, BT>;
-  // K-tile t + 2 of this tile, or past the end: the next tile's K-tile t + 2 - nk (persistent
-  // grid), else this tile's last one again (re-staged into a stage nobody reads)
-  const bool past = t + 2 >= nk;
-  const bool nxt = past && c.has_next;
-  const int tn2 = __builtin_amdgcn_readfirstlane(nxt ? t + 2 - nk : min(t + 2, nk - 1));
+  const int tn2 = __builtin_amdgcn_readfirstlane(min(t + 2, nk - 1));
   const unsigned kofsA = (unsigned)tn2 * c.stepA, kofsB = (unsigned)tn2 * c.stepB;
-  const i32x4_t srdA = nxt ? c.srdA_n : c.srdA, srdB = nxt ? c.srdB_n : c.srdB;
   const unsigned sb = c.sbase;
   sfor<2 * S::MH>([&](auto SS) {
     constexpr int s = SS;
@@ -389,9 +378,9 @@ __device__ __forceinline__ void ktile(f32x4_t (&acc)[8][NJ], Frags<NJ, AT, BT>& 
           constexpr int qa = d < 2 * NJ ? d / 2 : NJ + (d - 2 * NJ);
           constexpr bool isA = d < 2 * NJ ? (d % 2 == 0) : true;
           if constexpr (isA)
-            dma16<S::A_AT(CUR) + qa * 4 * PIECE>(srdA, c.voA[qa], kofsA, sb);
+            dma16<S::A_AT(CUR) + qa * 4 * PIECE>(c.srdA, c.voA[qa], kofsA, sb);
           else
-            dma16<S::B_AT(CUR) + (d / 2) * 4 * PIECE>(srdB, c.voB[d / 2], kofsB, sb);
+            dma16<S::B_AT(CUR) + (d / 2) * 4 * PIECE>(c.srdB, c.voB[d / 2], kofsB, sb);
         }
       });
     }
@@ -411,40 +400,25 @@ __device__ __forceinline__ void ktile(f32x4_t (&acc)[8][NJ], Frags<NJ, AT, BT>& 
 template <class E, int NJ, int EPI, bool AT, bool BT>
 __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(W4Args p) {
   using S = Sched<NJ, AT, BT>;
-  // the store / residual epilogues (GEN) stage through a 32 KiB region of their own after the
-  // stages (8 KiB per wave, 32 rows per pass), so a persistent workgroup's next tile can sit in the
-  // stages while this tile is stored; the special epilogues stage whole quadrants over the stages
-  constexpr bool GEN = EPI == W4_STORE || EPI == W4_RES;
-  constexpr int EPO = 2 * S::ST;  // GEN epilogue region
-  constexpr int LDS = GEN ? 2 * S::ST + 32768 : (2 * S::ST > 4 * 32768 ? 2 * S::ST : 4 * 32768);
+  constexpr int LDS = 2 * S::ST > 4 * 32768 ? 2 * S::ST : 4 * 32768;  // stages / epilogue staging
   __shared__ __attribute__((aligned(1024))) char smem[LDS];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid >> 1, wn = wid & 1;
   constexpr int BN = 32 * NJ, NW = 16 * NJ;
   const int ntiles = p.tiles_m * p.tiles_n;
-  const bool persist = GEN && p.persist;     // uniform
-  const int nsplit = (!persist && p.splits > 1) ? p.splits : 1;
-  const int ks = persist ? 0 : (int)blockIdx.x / ntiles;  // K slice of a split-K tile (0 without split)
-  int tb = persist ? (int)blockIdx.x : (int)blockIdx.x - ks * ntiles;  // output tile
+  const int nsplit = p.splits > 1 ? p.splits : 1;
+  const int ks = blockIdx.x / ntiles;        // K slice of a split-K tile (0 without split)
+  const int tb = blockIdx.x - ks * ntiles;   // output tile
+  const int2 tt = tile_of(tb, p.tiles_m, p.tiles_n, p.nfast);
+  const int tm = tt.x, tn = tt.y;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int f0 = tn * NW;  // W4_SWIGLU: first feature of the tile (NW features of w1 and of w3)
   // K-tiles in pairs; slice ks takes pairs [np * ks / S, np * (ks + 1) / S) (host: np >= S)
   const int npairs = p.K / (2 * BK);
   const int kp0 = npairs * ks / nsplit, kp1 = npairs * (ks + 1) / nsplit;
   const int nk = 2 * (kp1 - kp0);            // K-tiles of this workgroup (even)
   const long k0 = (long)kp0 * 2 * BK;        // its first k
-  // a tile's DMA sources (every per-lane offset below is the same for all tiles)
-  auto srd_a = [&](int m0x) {
-    return AT ? make_srd(p.a + m0x + k0 * p.lda) : make_srd(p.a + (long)m0x * p.lda + k0);
-  };
-  auto srd_b = [&](int n0x, int f0x) {
-    (void)f0x;
-    return BT ? make_srd(p.b + n0x + k0 * p.ldb)
-              : make_srd((EPI == W4_SWIGLU ? p.b : p.b + (long)n0x * p.ldb) + k0);
-  };
-  int2 tt = tile_of(tb, p.tiles_m, p.tiles_n, p.nfast);
-  int tm = tt.x, tn = tt.y;
-  int m0 = tm * BM, n0 = tn * BN;
-  int f0 = tn * NW;  // W4_SWIGLU: first feature of the tile (NW features of w1 and of w3)
 
   // LDS-DMA sources. Instruction q of wave w fills image piece P = q * 4 + w (bytes [P KiB, +1 KiB)),
   // lane L its 16 B at P KiB + 16 L; the lane's source is the element that image slot holds.
@@ -454,6 +428,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(W4Args p) {
   const int lrow = wid * 8 + (lane >> 3), lch = (lane & 7) ^ (lane >> 3);
   if constexpr (AT) {
     // [64 k][256 m], 512-B rows: piece P holds k-rows 2P, 2P + 1
+    c.srdA = make_srd(p.a + m0 + k0 * p.lda);
     c.stepA = (unsigned)(BK * p.lda * 2);
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
@@ -464,11 +439,13 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(W4Args p) {
     }
   } else {
     // [256 rows][64 k], 128-B rows: lane's 16-B chunk (lane & 7) holds global chunk (lane & 7) ^ (row & 7)
+    c.srdA = make_srd(p.a + (long)m0 * p.lda + k0);
     c.stepA = (unsigned)(BK * 2);
 #pragma unroll
     for (int q = 0; q < 8; ++q) c.voA[q] = (unsigned)(((q * 32 + lrow) * p.lda + lch * 8) * 2);
   }
   if constexpr (BT) {
+    c.srdB = make_srd(p.b + n0 + k0 * p.ldb);
     c.stepB = (unsigned)(BK * p.ldb * 2);
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
@@ -478,6 +455,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(W4Args p) {
       c.voB[q] = (unsigned)(((long)k * p.ldb + gc * 8) * 2);
     }
   } else {
+    c.srdB = make_srd((EPI == W4_SWIGLU ? p.b : p.b + (long)n0 * p.ldb) + k0);
     c.stepB = (unsigned)(BK * 2);
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
@@ -513,392 +491,310 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(W4Args p) {
     }
   }
 
-  c.srdA = srd_a(m0);
-  c.srdB = srd_b(n0, f0);
-  c.has_next = 0;
-
   f32x4_t acc[8][NJ];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   Frags<NJ, AT, BT> f;
 
-  // prologue: K-tiles 0 and 1 of the first tile in flight
+  // prologue: tiles 0 and 1 in flight, then tile 0's k-step-0 fragments
   c.sbase = __builtin_amdgcn_readfirstlane(c.lds0 + wid * PIECE);
   const unsigned sb = c.sbase;
   sfor<8>([&](auto Q) { dma16<S::A_AT(0) + Q * 4 * PIECE>(c.srdA, c.voA[Q], 0u, sb); });
   sfor<NJ>([&](auto Q) { dma16<S::B_AT(0) + Q * 4 * PIECE>(c.srdB, c.voB[Q], 0u, sb); });
   sfor<8>([&](auto Q) { dma16<S::A_AT(1) + Q * 4 * PIECE>(c.srdA, c.voA[Q], c.stepA, sb); });
   sfor<NJ>([&](auto Q) { dma16<S::B_AT(1) + Q * 4 * PIECE>(c.srdB, c.voB[Q], c.stepB, sb); });
-  bool first = true;
-  for (;;) {  // tiles of this workgroup: one without a persistent grid
-    const int tb_next = tb + (int)gridDim.x;
-    c.has_next = persist && tb_next < ntiles;
-    int2 ttn = make_int2(0, 0);
-    if (c.has_next) {
-      ttn = tile_of(tb_next, p.tiles_m, p.tiles_n, p.nfast);
-      c.srdA_n = srd_a(ttn.x * BM);
-      c.srdB_n = srd_b(ttn.y * BN, ttn.y * NW);
-    }
-    // K-tile 0 landed (1 may be in flight); after a persistent tile the drain already waited for
-    // both (and the epilogue's stores are in flight: not waited for here)
-    if (first) vmcnt<S::D>();
-    barrier();
-    sfor<S::R>([&](auto RR) { rd<NJ, AT, BT, 0, 0, RR>(f.a0, f.b0, c); });
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  vmcnt<S::D>();
+  barrier();
+  sfor<S::R>([&](auto RR) { rd<NJ, AT, BT, 0, 0, RR>(f.a0, f.b0, c); });
 
-    // the zeroed accumulators are MFMA sources next (VALU write -> MFMA SrcC wait states): the
-    // ties pin every zero write before the pad (the register allocator places copies and
-    // materialisations freely; an asm that "writes" the accumulators is a fence it cannot cross)
-    tie_acc(acc);
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_nop 4" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    // nk is even (K % 128, checked on the host): K-tiles in pairs so every stage offset is static,
-    // and ONE code path for every tile (the last two re-stage the last tile -- or stage the next
-    // tile's first two -- and read a dead next k-step): with a separate tail the register allocator
-    // placed the accumulators differently in the tail and copied them across with v_accvgpr_mov
-    // right behind the asm MFMAs that were still writing them (the compiler cannot see those as
-    // MFMAs) -> stale accumulators.
-    int t = 0;
-    do {
-      ktile<E, NJ, AT, BT, 0, true, true>(acc, f, t, nk, c);
-      ktile<E, NJ, AT, BT, 1, true, true>(acc, f, t + 1, nk, c);
-      t += 2;
-    } while (t < nk);
-    // Drain: the last two K-tiles' DMAs and the dead next-k-step reads land, and the last MFMAs
-    // finish before VALU reads the accumulators (the compiler does not see the asm as MFMAs, so it
-    // inserts no wait states; sched_barrier: register-only instructions may otherwise be hoisted
-    // above an asm).
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    // ... and the ties: the accumulators and fragments are (as far as the compiler knows) produced
-    // here, so no read or copy of an accumulator, and no reuse of a fragment register, can be
-    // placed above the drain (both happened at the loop exit without them: accumulators copied
-    // right behind the asm MFMAs still writing them; index math written into registers whose
-    // dead LDS reads had not returned yet)
-    tie_frags(f);
-    tie_acc(acc);
+  // the zeroed accumulators are MFMA sources next (VALU write -> MFMA SrcC wait states): the
+  // ties pin every zero write before the pad (the register allocator places copies and
+  // materialisations freely; an asm that "writes" the accumulators is a fence it cannot cross)
+  tie_acc(acc);
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_nop 4" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  // nk is even (K % 128, checked on the host): K-tiles in pairs so every stage offset is static,
+  // and ONE code path for every tile (the last two re-stage the last tile and read a dead next
+  // k-step): with a separate tail the register allocator placed the accumulators differently in
+  // the tail and copied them across with v_accvgpr_mov right behind the asm MFMAs that were still
+  // writing them (the compiler cannot see those as MFMAs) -> stale accumulators.
+  int t = 0;
+  do {
+    ktile<E, NJ, AT, BT, 0, true, true>(acc, f, t, nk, c);
+    ktile<E, NJ, AT, BT, 1, true, true>(acc, f, t + 1, nk, c);
+    t += 2;
+  } while (t < nk);
+  // Drain: the re-staging DMAs of the last two K-tiles and the dead next-k-step reads land, and
+  // the last MFMAs finish before VALU reads the accumulators (the compiler does not see the asm
+  // as MFMAs, so it inserts no wait states; sched_barrier: register-only instructions may
+  // otherwise be hoisted above an asm).
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  // ... and the ties: the accumulators and fragments are (as far as the compiler knows) produced
+  // here, so no read or copy of an accumulator, and no reuse of a fragment register, can be
+  // placed above the drain (both happened at the loop exit without them: accumulators copied
+  // right behind the asm MFMAs still writing them; index math written into registers whose
+  // dead LDS reads had not returned yet)
+  tie_frags(f);
+  tie_acc(acc);
 
-    // (the dW layout, k-major A, has no split-K: its tile grids fill the chip, and the extra live
-    // registers of the hand-off pushed its widest tile into scratch)
-    const float4* split_slot = nullptr;  // split-K consumer: slice 0's partial (uniform)
-    if constexpr ((EPI == W4_STORE || EPI == W4_RES) && !AT) {
-      if (nsplit > 1) {  // uniform (2 .. 8: host-checked)
-        // Static roles, wave-uniform control flow (no single-lane branches near the 256 live
-        // accumulators: those made the compiler copy them to VGPRs and spill): slices 0 .. S-2 (the
-        // lower block ids: dispatched first) park their partials and raise their flags; the last
-        // slice waits for all of them and adds them in slice order in its epilogue (fixed order:
-        // deterministic). A waiting workgroup never holds back a producer: the producers are
-        // dispatched ahead of it and wait on nothing.
-        constexpr long SLOT = 4L * 8 * NJ * 64;  // float4 per partial tile
-        float4* slot = reinterpret_cast<float4*>(p.ws) + ((long)tb * (nsplit - 1) + ks) * SLOT +
-                       (long)wid * (8 * NJ * 64) + lane;
-        int* flags = p.tick + (long)tb * 8;
-        if (ks < nsplit - 1) {
-          // stored straight from the AGPRs (asm "a" operands, no VGPR copies of the accumulators);
-          // 1 KiB per wave store, 4 stores per 4 KiB window of the base (13-bit signed immediate)
-  #pragma unroll
-          for (int i = 0; i < 8; ++i)
-  #pragma unroll
-            for (int j = 0; j < NJ; ++j)
-              asm volatile("global_store_dwordx4 %0, %1, off offset:%2"
-                           :
-                           : "v"(slot + (long)(i * NJ + (j & ~3)) * 64), "a"(acc[i][j]), "i"((j & 3) * 1024)
-                           : "memory");
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          __syncthreads();
-          if (wid == 0) {  // the whole wave (one address, one value)
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __hip_atomic_store(flags + ks, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          }
-          return;
-        }
-        if (wid == 0) {
-          // lane l watches slice (l & 7)'s flag; bounded (2^22 polls, a few seconds) so a broken
-          // hand-off cannot hang the GPU
-          int* fl = flags + (lane & 7);
-          const bool watch = (lane & 7) < nsplit - 1;
-          for (int n = 0; n < (1 << 22); ++n) {
-            const int v = __hip_atomic_load(fl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (__all(!watch || v != 0)) break;
-            __builtin_amdgcn_s_sleep(4);
-          }
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-          __hip_atomic_store(fl, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-armed (all 8)
-        }
+  // (the dW layout, k-major A, has no split-K: its tile grids fill the chip, and the extra live
+  // registers of the hand-off pushed its widest tile into scratch)
+  const float4* split_slot = nullptr;  // split-K consumer: slice 0's partial (uniform)
+  if constexpr ((EPI == W4_STORE || EPI == W4_RES) && !AT) {
+    if (nsplit > 1) {  // uniform (2 .. 8: host-checked)
+      // Static roles, wave-uniform control flow (no single-lane branches near the 256 live
+      // accumulators: those made the compiler copy them to VGPRs and spill): slices 0 .. S-2 (the
+      // lower block ids: dispatched first) park their partials and raise their flags; the last
+      // slice waits for all of them and adds them in slice order in its epilogue (fixed order:
+      // deterministic). A waiting workgroup never holds back a producer: the producers are
+      // dispatched ahead of it and wait on nothing.
+      constexpr long SLOT = 4L * 8 * NJ * 64;  // float4 per partial tile
+      float4* slot = reinterpret_cast<float4*>(p.ws) + ((long)tb * (nsplit - 1) + ks) * SLOT +
+                     (long)wid * (8 * NJ * 64) + lane;
+      int* flags = p.tick + (long)tb * 8;
+      if (ks < nsplit - 1) {
+        // stored straight from the AGPRs (asm "a" operands, no VGPR copies of the accumulators);
+        // 1 KiB per wave store, 4 stores per 4 KiB window of the base (13-bit signed immediate)
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+          for (int j = 0; j < NJ; ++j)
+            asm volatile("global_store_dwordx4 %0, %1, off offset:%2"
+                         :
+                         : "v"(slot + (long)(i * NJ + (j & ~3)) * 64), "a"(acc[i][j]), "i"((j & 3) * 1024)
+                         : "memory");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        split_slot = slot - (long)ks * SLOT;  // slice 0's partial; the epilogue adds them as it converts
+        if (wid == 0) {  // the whole wave (one address, one value)
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          __hip_atomic_store(flags + ks, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        return;
       }
+      if (wid == 0) {
+        // lane l watches slice (l & 7)'s flag; bounded (2^22 polls, a few seconds) so a broken
+        // hand-off cannot hang the GPU
+        int* fl = flags + (lane & 7);
+        const bool watch = (lane & 7) < nsplit - 1;
+        for (int n = 0; n < (1 << 22); ++n) {
+          const int v = __hip_atomic_load(fl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (__all(!watch || v != 0)) break;
+          __builtin_amdgcn_s_sleep(4);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        __hip_atomic_store(fl, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-armed (all 8)
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      split_slot = slot - (long)ks * SLOT;  // slice 0's partial; the epilogue adds them as it converts
     }
+  }
 
-    const int cc = lane & 15;
+  // ---- epilogue through LDS: quadrant rows of 256 B (NW * 2 used), chunk c at c ^ (row & 15)
+  barrier();  // every wave is done with the stages before they become epilogue staging
+  char* wl = smem + wid * 32768;
+  {
     const int lr = lane & 15, hc = lane >> 4;  // acc row, 4-column group of the fragment
-    float sq = 0.f;  // sum of squares of the stored values (p.part)
-    if constexpr (GEN) {
-      // ---- epilogue through this wave's 8 KiB of the GEN region, 32 quadrant rows per pass: rows
-      // of 256 B (NW * 2 used), 16-B chunk c at c ^ (row & 15)
-      char* wl = smem + EPO + wid * 8192;
 #pragma unroll
-      for (int pass = 0; pass < 4; ++pass) {
+    for (int i = 0; i < 8; ++i) {
+      const int m = i * 16 + lr;
+      // split-K: the partials of slices 0 .. S-2 summed in slice order, then + this slice's own
+      // accumulators (fragment order, one row of fragments at a time: the sums are consumed
+      // here, never all live at once)
+      float4 ps[NJ];
+      if (split_slot != nullptr) {
 #pragma unroll
-        for (int ii = 0; ii < 2; ++ii) {
-          const int i = 2 * pass + ii;
-          const int m = ii * 16 + lr;
-          // split-K: the partials of slices 0 .. S-2 summed in slice order, then + this slice's
-          // own accumulators (one row of fragments at a time: never all live at once)
-          float4 ps[NJ];
-          if (split_slot != nullptr) {
-#pragma unroll
-            for (int j = 0; j < NJ; ++j) ps[j] = split_slot[(i * NJ + j) * 64];
-            for (int sl = 1; sl < nsplit - 1; ++sl) {
-              const float4* q = split_slot + (long)sl * (4L * 8 * NJ * 64);
-#pragma unroll
-              for (int j = 0; j < NJ; ++j) {
-                const float4 tq = q[(i * NJ + j) * 64];
-                ps[j].x += tq.x;
-                ps[j].y += tq.y;
-                ps[j].z += tq.z;
-                ps[j].w += tq.w;
-              }
-            }
-          }
+        for (int j = 0; j < NJ; ++j) ps[j] = split_slot[(i * NJ + j) * 64];
+        for (int sl = 1; sl < nsplit - 1; ++sl) {
+          const float4* q = split_slot + (long)sl * (4L * 8 * NJ * 64);
 #pragma unroll
           for (int j = 0; j < NJ; ++j) {
-            const int ch = 2 * j + (hc >> 1);
-            f32x4_t v = acc[i][j];
-            if (split_slot != nullptr) {
-              v[0] = ps[j].x + v[0];
-              v[1] = ps[j].y + v[1];
-              v[2] = ps[j].z + v[2];
-              v[3] = ps[j].w + v[3];
-            }
-            uint2 pk;
-            pk.x = pk2<E>(v[0], v[1]);
-            pk.y = pk2<E>(v[2], v[3]);
-            *reinterpret_cast<uint2*>(wl + m * 256 + ((ch ^ (m & 15)) << 4) + (hc & 1) * 8) = pk;
+            const float4 t = q[(i * NJ + j) * 64];
+            ps[j].x += t.x;
+            ps[j].y += t.y;
+            ps[j].z += t.z;
+            ps[j].w += t.w;
           }
         }
-        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes landed
-        __builtin_amdgcn_wave_barrier();
-        if (cc < 2 * NJ) {
-#pragma unroll
-          for (int rr = 0; rr < 8; ++rr) {
-            const int row = rr * 4 + (lane >> 4);
-            uint4 v = *reinterpret_cast<const uint4*>(wl + row * 256 + ((cc ^ (row & 15)) << 4));
-            const long gm = m0 + wm * 128 + pass * 32 + row;
-            const int gn = n0 + wn * NW + cc * 8;
-            if constexpr (EPI == W4_RES) {
-              float a[8], r[8];
-              unpack8e<E>(v, a);
-              unpack8e<E>(*reinterpret_cast<const uint4*>(p.r + gm * p.ldr + gn), r);
-#pragma unroll
-              for (int q = 0; q < 8; ++q) a[q] += r[q];
-              v = pack8e<E>(a);
-            }
-            if (p.part != nullptr) {
-              float a[8];
-              unpack8e<E>(v, a);
-#pragma unroll
-              for (int q = 0; q < 8; ++q) sq = fmaf(a[q], a[q], sq);
-            }
-            if (!(p.dbg & 1)) *reinterpret_cast<uint4*>(p.c + gm * p.ldc + gn) = v;
-          }
-        }
-        __builtin_amdgcn_s_waitcnt(0xc07f);  // this pass's LDS reads done before the next writes
-        __builtin_amdgcn_wave_barrier();
       }
-    } else {
-      // ---- epilogue through LDS over the stages: quadrant rows of 256 B (NW * 2 used), chunk c
-      // at c ^ (row & 15)
-      barrier();  // every wave is done with the stages before they become epilogue staging
-      char* wl = smem + wid * 32768;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int ch = 2 * j + (hc >> 1);
+        f32x4_t v = acc[i][j];
+        if (split_slot != nullptr) {
+          v[0] = ps[j].x + v[0];
+          v[1] = ps[j].y + v[1];
+          v[2] = ps[j].z + v[2];
+          v[3] = ps[j].w + v[3];
+        }
+        uint2 pk;
+        pk.x = pk2<E>(v[0], v[1]);
+        pk.y = pk2<E>(v[2], v[3]);
+        *reinterpret_cast<uint2*>(wl + m * 256 + ((ch ^ (m & 15)) << 4) + (hc & 1) * 8) = pk;
+      }
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes landed
+  __builtin_amdgcn_wave_barrier();
+  const int cc = lane & 15;
+  float sq = 0.f;  // sum of squares of the stored values (p.part)
+  if constexpr (EPI == W4_SWIGLU_BWD) {
+    // dgu from da (LDS) and the saved gu (global): the gu rows of 16 tile rows are loaded before
+    // any is used (the fragment registers are free now), so the epilogue waits on HBM latency twice
+    // per tile instead of once per 4 rows
+    if (cc < 2 * NJ) {
+      const int gn = n0 + wn * NW + cc * 8;
+#pragma unroll
+      for (int hb = 0; hb < 2; ++hb) {
+        uint4 g16[16], u16[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const long gm = m0 + wm * 128 + (hb * 16 + q) * 4 + (lane >> 4);
+          g16[q] = *reinterpret_cast<const uint4*>(p.r + gm * p.ldr + gn);
+          u16[q] = *reinterpret_cast<const uint4*>(p.r + gm * p.ldr + p.ffn + gn);
+        }
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const int row = (hb * 16 + q) * 4 + (lane >> 4);
+          const long gm = m0 + wm * 128 + row;
+          const uint4 v = *reinterpret_cast<const uint4*>(wl + row * 256 + ((cc ^ (row & 15)) << 4));
+          // v = da (bf16, as the unfused path's GEMM output) for features gn .. gn + 7 of token gm:
+          // dg, du from the saved g = gu[gm, gn], u = gu[gm, F + gn] (swiglu_grad, common.h)
+          float d8[8], g8[8], u8[8], dg[8], du[8];
+          unpack8e<E>(v, d8);
+          unpack8e<E>(g16[q], g8);
+          unpack8e<E>(u16[q], u8);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) swiglu_grad(g8[e], u8[e], d8[e], p.exact, dg[e], du[e]);
+          *reinterpret_cast<uint4*>(p.c + gm * p.ldc + gn) = pack8e<E>(dg);
+          *reinterpret_cast<uint4*>(p.c + gm * p.ldc + p.ffn + gn) = pack8e<E>(du);
+        }
+      }
+    }
+  } else if (cc < 2 * NJ) {
+#pragma unroll 4
+    for (int rr = 0; rr < 32; ++rr) {
+      const int row = rr * 4 + (lane >> 4);
+      uint4 v = *reinterpret_cast<const uint4*>(wl + row * 256 + ((cc ^ (row & 15)) << 4));
+      const long gm = m0 + wm * 128 + row;
+      // W4_SWIGLU: wave column half 0 holds g (gu columns [0, F)), half 1 holds u ([F, 2F))
+      const int gn = EPI == W4_SWIGLU ? (wn ? p.ffn : 0) + f0 + cc * 8 : n0 + wn * NW + cc * 8;
+      if constexpr (EPI == W4_RES) {
+        float a[8], r[8];
+        unpack8e<E>(v, a);
+        unpack8e<E>(*reinterpret_cast<const uint4*>(p.r + gm * p.ldr + gn), r);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) a[q] += r[q];
+        v = pack8e<E>(a);
+      } else if constexpr (EPI == W4_ROPE) {
+        if (gn < p.rope_cols) {
+          // 8 columns = 4 interleaved (x0, x1) pairs of one head: rotated in fp32 by the bf16
+          // projection output, as the separate kernel did (rope.hip / model.py:121-126)
+          const int pos = (int)(gm % p.rope_seq);
+          const int i0 = (gn % p.rope_hd) >> 1;
+          const float* cs = p.cos_t + (long)pos * (p.rope_hd >> 1) + i0;
+          const float* sn = p.sin_t + (long)pos * (p.rope_hd >> 1) + i0;
+          const float4 c4 = *reinterpret_cast<const float4*>(cs);
+          const float4 s4 = *reinterpret_cast<const float4*>(sn);
+          float a[8];
+          unpack8e<E>(v, a);
+          const float cv[4] = {c4.x, c4.y, c4.z, c4.w}, sv[4] = {s4.x, s4.y, s4.z, s4.w};
+          float o[8];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            o[2 * q] = a[2 * q] * cv[q] - a[2 * q + 1] * sv[q];
+            o[2 * q + 1] = a[2 * q] * sv[q] + a[2 * q + 1] * cv[q];
+          }
+          v = pack8e<E>(o);
+        }
+      }
+      if (p.part != nullptr) {
+        float a[8];
+        unpack8e<E>(v, a);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) sq = fmaf(a[q], a[q], sq);
+      }
+      if (!(p.dbg & 1)) *reinterpret_cast<uint4*>(p.c + gm * p.ldc + gn) = v;
+    }
+  }
+  if (p.part != nullptr) {  // uniform: one partial per tile, fixed order (deterministic)
+    sq = wave_sum(sq);
+    __syncthreads();  // every wave is done with its staging quadrant
+    float* red = reinterpret_cast<float*>(smem);
+    if (lane == 0) red[wid] = sq;
+    __syncthreads();
+    if (tid == 0) p.part[tn * p.tiles_m + tm] = (red[0] + red[1]) + (red[2] + red[3]);
+    // a sink's slice can hold more slots than this tile grid (sized for the smallest tile, and
+    // written whole by the fallback pass): stale partials there would enter the global norm
+    if (tb == 0)  // (tile 0's epilogue workgroup: with split-K its first half exits early)
+      for (int i = ntiles + tid; i < p.part_n; i += NT) p.part[i] = 0.f;
+  }
+  if constexpr (EPI == W4_SWIGLU) {
+    // a = silu(g) * u from the parked bf16 g / u quadrants (the values just stored to gu, so a is
+    // bitwise what swiglu_fwd_t computes from gu): wave (wm, wn) takes rows [64 wn, 64 wn + 64) of
+    // its row half, writes a row-major and back over g in LDS, then all waves store a^T
+    __syncthreads();
+    char* gl = smem + (wm * 2) * 32768;      // g quadrant of this row half
+    char* ul = smem + (wm * 2 + 1) * 32768;  // u quadrant
+    if (cc < 2 * NJ) {
+#pragma unroll 4
+      for (int rr = 0; rr < 16; ++rr) {
+        const int row = wn * 64 + rr * 4 + (lane >> 4);
+        const int off = row * 256 + ((cc ^ (row & 15)) << 4);
+        float g8[8], u8[8], a8[8];
+        unpack8e<E>(*reinterpret_cast<const uint4*>(gl + off), g8);
+        unpack8e<E>(*reinterpret_cast<const uint4*>(ul + off), u8);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) a8[q] = g8[q] * sigmoid_f(g8[q], p.exact) * u8[q];
+        const uint4 av = pack8e<E>(a8);
+        *reinterpret_cast<uint4*>(p.act + (m0 + wm * 128 + row) * (long)p.ffn + f0 + cc * 8) = av;
+        *reinterpret_cast<uint4*>(gl + off) = av;
+      }
+    }
+    if (p.actT == nullptr) return;  // uniform
+    __syncthreads();
+    // a^T [F, M]: a thread takes 8 tokens x 8 features (8 row-chunk LDS reads, feature chunk
+    // fastest across lanes: distinct XOR-swizzled chunks, conflict-free), transposes the block in
+    // registers and stores 8 16-B pieces (8 tokens of one feature each)
+    constexpr int CH = 2 * NJ;  // 8-feature chunks per tile row
+    for (int k = tid; k < 2 * 16 * CH; k += NT) {
+      const int fc = k % CH, tg = (k / CH) % 16, hf = k / (16 * CH);
+      const char* al = smem + (hf * 2) * 32768;  // a of row half hf (written over g)
+      uint16_t e[8][8];                          // [token][feature]
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        const int m = i * 16 + lr;
+        const int row = tg * 8 + i;
+        const uint4 v = *reinterpret_cast<const uint4*>(al + row * 256 + ((fc ^ (row & 15)) << 4));
+        const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-          const int ch = 2 * j + (hc >> 1);
-          const f32x4_t v = acc[i][j];
-          uint2 pk;
-          pk.x = pk2<E>(v[0], v[1]);
-          pk.y = pk2<E>(v[2], v[3]);
-          *reinterpret_cast<uint2*>(wl + m * 256 + ((ch ^ (m & 15)) << 4) + (hc & 1) * 8) = pk;
+        for (int q = 0; q < 4; ++q) {
+          e[i][2 * q] = (uint16_t)(wv[q] & 0xffffu);
+          e[i][2 * q + 1] = (uint16_t)(wv[q] >> 16);
         }
       }
-      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes landed
-      __builtin_amdgcn_wave_barrier();
-      if constexpr (EPI == W4_SWIGLU_BWD) {
-        // dgu from da (LDS) and the saved gu (global): the gu rows of 16 tile rows are loaded before
-        // any is used (the fragment registers are free now), so the epilogue waits on HBM latency twice
-        // per tile instead of once per 4 rows
-        if (cc < 2 * NJ) {
-          const int gn = n0 + wn * NW + cc * 8;
-    #pragma unroll
-          for (int hb = 0; hb < 2; ++hb) {
-            uint4 g16[16], u16[16];
-    #pragma unroll
-            for (int q = 0; q < 16; ++q) {
-              const long gm = m0 + wm * 128 + (hb * 16 + q) * 4 + (lane >> 4);
-              g16[q] = *reinterpret_cast<const uint4*>(p.r + gm * p.ldr + gn);
-              u16[q] = *reinterpret_cast<const uint4*>(p.r + gm * p.ldr + p.ffn + gn);
-            }
-    #pragma unroll
-            for (int q = 0; q < 16; ++q) {
-              const int row = (hb * 16 + q) * 4 + (lane >> 4);
-              const long gm = m0 + wm * 128 + row;
-              const uint4 v = *reinterpret_cast<const uint4*>(wl + row * 256 + ((cc ^ (row & 15)) << 4));
-              // v = da (bf16, as the unfused path's GEMM output) for features gn .. gn + 7 of token gm:
-              // dg, du from the saved g = gu[gm, gn], u = gu[gm, F + gn] (swiglu_grad, common.h)
-              float d8[8], g8[8], u8[8], dg[8], du[8];
-              unpack8e<E>(v, d8);
-              unpack8e<E>(g16[q], g8);
-              unpack8e<E>(u16[q], u8);
-    #pragma unroll
-              for (int e = 0; e < 8; ++e) swiglu_grad(g8[e], u8[e], d8[e], p.exact, dg[e], du[e]);
-              *reinterpret_cast<uint4*>(p.c + gm * p.ldc + gn) = pack8e<E>(dg);
-              *reinterpret_cast<uint4*>(p.c + gm * p.ldc + p.ffn + gn) = pack8e<E>(du);
-            }
-          }
-        }
-      } else if (cc < 2 * NJ) {
-    #pragma unroll 4
-        for (int rr = 0; rr < 32; ++rr) {
-          const int row = rr * 4 + (lane >> 4);
-          uint4 v = *reinterpret_cast<const uint4*>(wl + row * 256 + ((cc ^ (row & 15)) << 4));
-          const long gm = m0 + wm * 128 + row;
-          // W4_SWIGLU: wave column half 0 holds g (gu columns [0, F)), half 1 holds u ([F, 2F))
-          const int gn = EPI == W4_SWIGLU ? (wn ? p.ffn : 0) + f0 + cc * 8 : n0 + wn * NW + cc * 8;
-          if constexpr (EPI == W4_RES) {
-            float a[8], r[8];
-            unpack8e<E>(v, a);
-            unpack8e<E>(*reinterpret_cast<const uint4*>(p.r + gm * p.ldr + gn), r);
-    #pragma unroll
-            for (int q = 0; q < 8; ++q) a[q] += r[q];
-            v = pack8e<E>(a);
-          } else if constexpr (EPI == W4_ROPE) {
-            if (gn < p.rope_cols) {
-              // 8 columns = 4 interleaved (x0, x1) pairs of one head: rotated in fp32 by the bf16
-              // projection output, as the separate kernel did (rope.hip / model.py:121-126)
-              const int pos = (int)(gm % p.rope_seq);
-              const int i0 = (gn % p.rope_hd) >> 1;
-              const float* cs = p.cos_t + (long)pos * (p.rope_hd >> 1) + i0;
-              const float* sn = p.sin_t + (long)pos * (p.rope_hd >> 1) + i0;
-              const float4 c4 = *reinterpret_cast<const float4*>(cs);
-              const float4 s4 = *reinterpret_cast<const float4*>(sn);
-              float a[8];
-              unpack8e<E>(v, a);
-              const float cv[4] = {c4.x, c4.y, c4.z, c4.w}, sv[4] = {s4.x, s4.y, s4.z, s4.w};
-              float o[8];
-    #pragma unroll
-              for (int q = 0; q < 4; ++q) {
-                o[2 * q] = a[2 * q] * cv[q] - a[2 * q + 1] * sv[q];
-                o[2 * q + 1] = a[2 * q] * sv[q] + a[2 * q + 1] * cv[q];
-              }
-              v = pack8e<E>(o);
-            }
-          }
-          if (p.part != nullptr) {
-            float a[8];
-            unpack8e<E>(v, a);
-    #pragma unroll
-            for (int q = 0; q < 8; ++q) sq = fmaf(a[q], a[q], sq);
-          }
-          if (!(p.dbg & 1)) *reinterpret_cast<uint4*>(p.c + gm * p.ldc + gn) = v;
-        }
+      bf16_t* dst = p.actT + (long)(f0 + fc * 8) * p.M + m0 + hf * 128 + tg * 8;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        uint4 o;
+        o.x = e[0][j] | ((uint32_t)e[1][j] << 16);
+        o.y = e[2][j] | ((uint32_t)e[3][j] << 16);
+        o.z = e[4][j] | ((uint32_t)e[5][j] << 16);
+        o.w = e[6][j] | ((uint32_t)e[7][j] << 16);
+        *reinterpret_cast<uint4*>(dst + (long)j * p.M) = o;
       }
     }
-    if (p.part != nullptr) {  // uniform: one partial per tile, fixed order (deterministic)
-      sq = wave_sum(sq);
-      // wave w's sum in the first word of its (finished) epilogue staging: the GEN region (the
-      // stages may hold the next tile), or the quadrant over the stages
-      constexpr int RS = GEN ? 8192 : 32768;
-      float* red = reinterpret_cast<float*>(smem + (GEN ? EPO : 0));
-      if (!GEN) __syncthreads();  // (quadrants are read across waves by the special epilogues)
-      if (lane == 0) red[wid * (RS / 4)] = sq;
-      __syncthreads();
-      if (tid == 0)
-        p.part[tn * p.tiles_m + tm] = (red[0] + red[RS / 4]) + (red[2 * (RS / 4)] + red[3 * (RS / 4)]);
-      // a sink's slice can hold more slots than this tile grid (sized for the smallest tile, and
-      // written whole by the fallback pass): stale partials there would enter the global norm
-      if (tb == 0)  // (tile 0's epilogue workgroup: with split-K its first slices exit early)
-        for (int i = ntiles + tid; i < p.part_n; i += NT) p.part[i] = 0.f;
-      __syncthreads();  // red[] is free for the next tile
-    }
-    if constexpr (EPI == W4_SWIGLU) {
-      // a = silu(g) * u from the parked bf16 g / u quadrants (the values just stored to gu, so a is
-      // bitwise what swiglu_fwd_t computes from gu): wave (wm, wn) takes rows [64 wn, 64 wn + 64) of
-      // its row half, writes a row-major and back over g in LDS, then all waves store a^T
-      __syncthreads();
-      char* gl = smem + (wm * 2) * 32768;      // g quadrant of this row half
-      char* ul = smem + (wm * 2 + 1) * 32768;  // u quadrant
-      if (cc < 2 * NJ) {
-  #pragma unroll 4
-        for (int rr = 0; rr < 16; ++rr) {
-          const int row = wn * 64 + rr * 4 + (lane >> 4);
-          const int off = row * 256 + ((cc ^ (row & 15)) << 4);
-          float g8[8], u8[8], a8[8];
-          unpack8e<E>(*reinterpret_cast<const uint4*>(gl + off), g8);
-          unpack8e<E>(*reinterpret_cast<const uint4*>(ul + off), u8);
-  #pragma unroll
-          for (int q = 0; q < 8; ++q) a8[q] = g8[q] * sigmoid_f(g8[q], p.exact) * u8[q];
-          const uint4 av = pack8e<E>(a8);
-          *reinterpret_cast<uint4*>(p.act + (m0 + wm * 128 + row) * (long)p.ffn + f0 + cc * 8) = av;
-          *reinterpret_cast<uint4*>(gl + off) = av;
-        }
-      }
-      if (p.actT == nullptr) return;  // uniform
-      __syncthreads();
-      // a^T [F, M]: a thread takes 8 tokens x 8 features (8 row-chunk LDS reads, feature chunk
-      // fastest across lanes: distinct XOR-swizzled chunks, conflict-free), transposes the block in
-      // registers and stores 8 16-B pieces (8 tokens of one feature each)
-      constexpr int CH = 2 * NJ;  // 8-feature chunks per tile row
-      for (int k = tid; k < 2 * 16 * CH; k += NT) {
-        const int fc = k % CH, tg = (k / CH) % 16, hf = k / (16 * CH);
-        const char* al = smem + (hf * 2) * 32768;  // a of row half hf (written over g)
-        uint16_t e[8][8];                          // [token][feature]
-  #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const int row = tg * 8 + i;
-          const uint4 v = *reinterpret_cast<const uint4*>(al + row * 256 + ((fc ^ (row & 15)) << 4));
-          const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
-  #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            e[i][2 * q] = (uint16_t)(wv[q] & 0xffffu);
-            e[i][2 * q + 1] = (uint16_t)(wv[q] >> 16);
-          }
-        }
-        bf16_t* dst = p.actT + (long)(f0 + fc * 8) * p.M + m0 + hf * 128 + tg * 8;
-  #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          uint4 o;
-          o.x = e[0][j] | ((uint32_t)e[1][j] << 16);
-          o.y = e[2][j] | ((uint32_t)e[3][j] << 16);
-          o.z = e[4][j] | ((uint32_t)e[5][j] << 16);
-          o.w = e[6][j] | ((uint32_t)e[7][j] << 16);
-          *reinterpret_cast<uint4*>(dst + (long)j * p.M) = o;
-        }
-      }
-    }
-    if (!c.has_next) break;
-    tb = tb_next;
-    tm = ttn.x;
-    tn = ttn.y;
-    m0 = tm * BM;
-    n0 = tn * BN;
-    f0 = tn * NW;
-    c.srdA = c.srdA_n;
-    c.srdB = c.srdB_n;
-    first = false;
   }
 }
 
 template <class E, int NJ, bool AT, bool BT>
 void launch_nj(const W4Args& p, int epi, hipStream_t st) {
-  const dim3 g(p.persist ? p.persist : p.tiles_m * p.tiles_n * (p.splits > 1 ? p.splits : 1));
+  const dim3 g(p.tiles_m * p.tiles_n * (p.splits > 1 ? p.splits : 1));
   if constexpr (!AT && !BT) {
     if (epi == W4_ROPE) {
       hipLaunchKernelGGL((gemm_w4_kernel<E, NJ, W4_ROPE, false, false>), g, dim3(NT), 0, st, p);

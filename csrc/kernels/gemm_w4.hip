@@ -123,28 +123,6 @@ int* splitk_ticks(const c10::Device& dev, hipStream_t st, long n) {
 // stream). Falls back to one workgroup per tile where the split cannot run.
 int g_dbg = 0;  // timing probes (gemm_w4_set_dbg): W4Args::dbg of every launch
 
-// Persistent grid for the store / residual epilogues without split (gemm_w4.h W4Args::persist):
-// a tile grid of more than one round runs as one workgroup per CU walking its tiles, the next
-// tile's first K-tiles staged during the current one's last. set_persist(0) turns it off (A/B).
-int g_persist = 1;
-
-int cu_count() {
-  static int n = [] {
-    int dev = 0, v = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      return 256;
-    return v > 0 ? v : 256;
-  }();
-  return n;
-}
-
-void setup_persist(W4Args& p, int epi) {
-  p.persist = 0;
-  const long tiles = (long)p.tiles_m * p.tiles_n;
-  const int g = cu_count() / 8 * 8;  // a multiple of 8: workgroup b stays on XCD b % 8 for every tile
-  if (g_persist && p.splits <= 1 && (epi == W4_STORE || epi == W4_RES) && g >= 8 && tiles > g) p.persist = g;
-}
-
 void setup_split(W4Args& p, int splits, int nj, const at::Tensor& like, at::Tensor& ws_hold) {
   p.dbg = g_dbg;
   p.splits = 1;
@@ -213,7 +191,6 @@ at::Tensor gemm_nt_w4(const at::Tensor& a, const at::Tensor& b, const std::optio
   }
   at::Tensor ws;
   setup_split(p, pl.splits, NJ, a, ws);
-  setup_persist(p, epi);
   launch(a.scalar_type(), NJ, p, epi, ft_stream());
   FT_LAUNCH_CHECK();
   return c;
@@ -278,7 +255,6 @@ at::Tensor gemm_w4_ex(const at::Tensor& a, bool a_t, const at::Tensor& b, bool b
   }
   at::Tensor ws;
   setup_split(p, pl.splits, NJ, a, ws);
-  setup_persist(p, accumulate ? W4_RES : W4_STORE);
   launch(a.scalar_type(), NJ, p, accumulate ? W4_RES : W4_STORE, ft_stream(), a_t, b_t);
   FT_LAUNCH_CHECK();
   return c;
@@ -423,8 +399,6 @@ void gemm_w4_set_splitk(int64_t mode) { g_splitk_mode = (int)mode; }
 // global stores (the output is left unwritten)
 void gemm_w4_set_dbg(int64_t v) { g_dbg = (int)v; }
 
-void gemm_w4_set_persist(int64_t on) { g_persist = (int)on; }
-
 // (tile width / 32, splits) the automatic choice takes for C[M, N] over a K-deep sum
 std::vector<int64_t> gemm_w4_plan(int64_t M, int64_t N, int64_t K, bool a_t, bool b_t) {
   const Plan pl = pick_plan(M, N, K, a_t, b_t);
@@ -441,7 +415,6 @@ TORCH_LIBRARY_FRAGMENT(ftamd, m) {
   m.def("gemm_w4_plan(int M, int N, int K, bool a_t=False, bool b_t=False) -> int[]", &gemm_w4_plan);
   m.def("gemm_w4_set_splitk(int mode) -> ()", &gemm_w4_set_splitk);
   m.def("gemm_w4_set_dbg(int v) -> ()", &gemm_w4_set_dbg);
-  m.def("gemm_w4_set_persist(int on) -> ()", &gemm_w4_set_persist);
   m.def("gemm_qkv_rope_w4(Tensor x, Tensor w, Tensor cos, Tensor sin, int seq, int hq, int hkv, int d) -> Tensor",
         &gemm_qkv_rope_w4);
   m.def("gemm_w4_pick(int M, int N) -> int", &gemm_w4_pick);

@@ -38,9 +38,6 @@ def main():
     K_ = kernels()
     r = lambda *s: (torch.rand(*s, device="cuda") * 2 - 1).bfloat16()  # noqa: E731
     Ks = [512, 1024, 2048, 4096, 8192]
-    persist = os.environ.get("W4_PROBE_PERSIST", "1") != "0"
-    K_.gemm_w4_set_persist(1 if persist else 0)
-    print(f"persistent grid: {'on' if persist else 'off'}", flush=True)
     for M, N in ((4096, 4096), (8192, 8192)):
         rounds = (M // 256) * (N // 256) // 256
         for layout in ("fwd", "dx", "dw"):

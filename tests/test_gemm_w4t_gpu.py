@@ -201,46 +201,3 @@ def test_split_k_8b_head_dx_vs_fp32():
     ref = a[rows].float() @ b.float()
     assert rel(c[rows], ref) < 4e-3
     assert torch.equal(c, K().gemm_w4_ex(a, False, b, True, M, N, Kd, None, False, None, 8, 2))
-
-
-# ---- persistent grid (gemm_w4.h W4Args::persist): one workgroup per CU walks its tiles, the next
-# tile's first K-tiles staged during the current one's last; the per-tile math is unchanged, so the
-# results must equal the one-workgroup-per-tile launch bit for bit (store, accumulate, partials)
-@pytest.mark.parametrize("layout", ["fwd", "dx", "dw"])
-@pytest.mark.parametrize("M,N,Kd,nj", [(4096, 8192, 512, 8), (8192, 4096, 256, 8), (2048, 14336, 384, 7),
-                                       (6144, 4096, 256, 4)])
-def test_persistent_grid_bitwise(layout, M, N, Kd, nj):
-    torch.manual_seed(M + N + Kd + nj)
-    if layout == "fwd":
-        a, b = rnd(M, Kd), rnd(N, Kd)
-        run = lambda out=None, acc=False, part=None: K().gemm_nt_w4(a, b, out, out if acc else None, nj, 1)  # noqa: E731
-        ref = a.float() @ b.float().t()
-    else:
-        at = layout == "dw"
-        a = rnd(Kd, M) if at else rnd(M, Kd)
-        b = rnd(Kd, N)
-        run = lambda out=None, acc=False, part=None: K().gemm_w4_ex(a, at, b, True, M, N, Kd, out, acc, part, nj, 1)  # noqa: E731
-        ref = (a.float().t() if at else a.float()) @ b.float()
-    tiles = (M // 256) * (N // (32 * nj))
-    assert tiles > 256  # more than one round: the persistent grid takes it
-    outs = {}
-    c0 = rnd(M, N)
-    for pers in (0, 1):
-        K().gemm_w4_set_persist(pers)
-        try:
-            c = run()
-            c2 = c0.clone()
-            part = torch.full((tiles + 7,), -1.0, device="cuda") if layout == "dw" else None
-            run(c2, True, part)
-        finally:
-            K().gemm_w4_set_persist(1)
-        outs[pers] = (c, c2, part)
-    (c_a, r_a, p_a), (c_b, r_b, p_b) = outs[0], outs[1]
-    assert rel(c_b, ref) < 4e-3
-    assert torch.equal(c_a, c_b) and torch.equal(r_a, r_b)
-    assert rel(r_b, ref + c0.float()) < 4e-3
-    if layout == "dw":
-        assert torch.equal(p_a, p_b)
-        assert torch.all(p_b[tiles:] == 0.0)
-        want = r_b.float().pow(2).sum().item()
-        assert abs(p_b[:tiles].double().sum().item() - want) <= 1e-5 * want
