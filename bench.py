@@ -64,8 +64,8 @@ def parse():
     ap.add_argument("--grad-accum", type=int, default=1, help="micro-batches per optimizer step")
     ap.add_argument("--no-exposed-comm", action="store_true", help="skip the DP exposed-collective estimate")
     ap.add_argument("--graph", action="store_true",
-                    help="1 GPU: replay each step as one HIP graph (optimizer of step k with forward/backward "
-                         "of step k+1): for launch-bound presets (gpt2-small / gpt2-medium)")
+                    help="replay each step as one HIP graph (optimizer of step k with forward/backward of "
+                         "step k+1, the RCCL bucket collectives captured under DP): launch-bound presets")
     ap.add_argument("--device", default="cuda")
     ap.add_argument("--dp-mode", default="", choices=["", "allreduce", "zero1"])
     ap.add_argument("--dp-reduce-dtype", default="native", choices=["native", "bf16", "fp32"],
@@ -193,8 +193,12 @@ def main():
 
     graphed = None
     if a.graph:
-        if world > 1 or K > 1 or dev.type != "cuda":
-            raise SystemExit("--graph: one GPU, no gradient accumulation")
+        if K > 1 or dev.type != "cuda":
+            raise SystemExit("--graph: GPU ranks, no gradient accumulation")
+        if red.mode == "zero1":
+            # ZeRO-1's gated parameter all-gathers crashed under capture (1-rank RCCL, round 5):
+            # the captured DP step is the all-reduce mode's
+            raise SystemExit("--graph under data parallelism: --dp-mode allreduce")
         from fault_tolerant_llm_training_amd.graphs import GraphedStep
 
         def fwd_bwd(tok, lab):
@@ -287,12 +291,11 @@ def main():
         "rccl_version": topo["rccl_version"],
     }
     if sampler is not None:
-        # board power / shader clock over the timed region (rank 0's GPU): the step runs at the
-        # power limit, so these tell a hotter or lower-clocked box from slower code
+        # board power / shader clock over the timed region (rank 0's GPU): they tell a hotter or
+        # lower-clocked box from slower code. (No clock-normalised step time: across boxes the step
+        # moved ~0.45 % per 1 % of sclk, not 1:1 -- AdamW and the epilogues are memory-bound --
+        # docs/PERFORMANCE.md "Box-to-box variance"; compare code on one box: scripts/so_ab.sh.)
         out.update(sampler.summary())
-        sc = out.get("sclk_mhz_p50")
-        if sc:
-            out["ms_per_step_at_2000mhz"] = round(ms * sc / 2000.0, 2)
     if a.dp_reduce_dtype == "fp32":
         out["dp_reduce_dtype"] = "fp32"
     if graphed is not None:

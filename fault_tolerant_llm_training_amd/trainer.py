@@ -268,20 +268,23 @@ def train(args) -> int:
         # The reference compiles the model (train.py:61-63) to cut launch overhead and fuse ops.
         # Here the ops are already fused gfx950 kernels; what is left to "compile" is the launch
         # sequence, and the MI355X-native form of that is the whole-step HIP graph (--hip-graph):
-        # on one GPU without gradient accumulation --compile turns it on. Elsewhere the graph
-        # cannot capture the step (collectives / host-side accumulation), so the flag is accepted
-        # and logged as not applied.
-        graphable = model_dtype in (torch.bfloat16, torch.float16, torch.float32)
-        if device.type == "cuda" and not info.distributed and max(1, int(args.grad_accum)) == 1 and graphable:
+        # on GPU ranks without gradient accumulation --compile turns it on (under DP the bucket
+        # collectives are captured into the graph; the per-step vote stays on the host, between
+        # replays). Host-side accumulation or the fp64 path cannot be captured: there the flag
+        # is accepted and logged as not applied.
+        graphable = model_dtype in (torch.bfloat16, torch.float16, torch.float32) and not (
+            info.distributed and args.dp_mode != "allreduce")
+        if device.type == "cuda" and max(1, int(args.grad_accum)) == 1 and graphable:
             logger.info("Using `torch.compile`")
             logger.info("`torch.compile` -> whole-step HIP graph capture (--hip-graph): the step's "
                         "kernel launches are recorded once and replayed")
             args.hip_graph = True
         else:
             logger.info("Using `torch.compile` — accepted for CLI compatibility, not applied: the step "
-                        "already runs fused gfx950 kernels and the whole-step HIP graph needs one GPU "
+                        "already runs fused gfx950 kernels and the whole-step HIP graph needs GPU ranks "
                         "without gradient accumulation, in a dtype the HIP kernels run (bf16/fp16/fp32: "
-                        "the fp64 composed path synchronises with the host inside the step)")
+                        "the fp64 composed path synchronises with the host inside the step), and under "
+                        "data parallelism --dp-mode allreduce")
     model.train()
 
     # AdamW moments default to the model dtype like the reference, except under fp16: the second
@@ -513,10 +516,12 @@ def train(args) -> int:
 
     graphed = None
     if args.hip_graph:
-        if info.distributed or K > 1 or device.type != "cuda" \
-                or model_dtype not in (torch.bfloat16, torch.float16, torch.float32):
-            raise ValueError("--hip-graph: one GPU without a process group, --grad-accum 1, --device cuda, "
-                             "--model-dtype bf16/fp16/fp32")
+        if K > 1 or device.type != "cuda" or model_dtype not in (torch.bfloat16, torch.float16, torch.float32):
+            raise ValueError("--hip-graph: --grad-accum 1, --device cuda, --model-dtype bf16/fp16/fp32")
+        if reducer.mode == "zero1":
+            # ZeRO-1's gated parameter all-gathers crashed under stream capture (1-rank RCCL test,
+            # round 5): the captured DP step is the all-reduce mode's
+            raise ValueError("--hip-graph under data parallelism: --dp-mode allreduce")
         from .graphs import GraphedStep
 
         inv_dev = torch.empty(1, dtype=torch.float32, device=device)  # static input of the graph
