@@ -468,9 +468,14 @@ __global__ __launch_bounds__(64 * NW * SPLIT, 8 / (NW * SPLIT)) void flash_fwd_k
 template <class E, int D, int NW = 4>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void flash_fwd_pipe_kernel(
     const bf16_t* __restrict__ qk, const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out,
-    float* __restrict__ lse2, int B, int S, int Hq, int Hkv, float sl2, long ldqk_) {
+    float* __restrict__ lse2, int B, int S, int Hq, int Hkv, float sl2, long ldqk_,
+    long long* __restrict__ prof) {
   constexpr int BM = 32 * NW, BN = 64, KS = D / 16, NDB = D / 32;
   constexpr int TILE = BN * D * 2;
+  // timing probe (flash_set_fwd_prof; scripts/flash_fwd_timeline.py): 100 MHz wall clock at
+  // entry / after the prologue / after the key loop / after the stores, and the CU the block ran on
+  long long pt0 = 0, pt1 = 0, pt2 = 0;
+  if (prof) pt0 = __builtin_amdgcn_s_memrealtime();
   __shared__ __attribute__((aligned(16))) char kb0[TILE];
   __shared__ __attribute__((aligned(16))) char kb1[TILE];
   __shared__ __attribute__((aligned(16))) char vb0[TILE];
@@ -625,6 +630,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void flash_fwd_pipe_kernel(
     rescale(rowmax(sa, 0, std::false_type{}));
   }
   __syncthreads();  // K(0) read by every wave before K(2) lands in kb0
+  if (prof) pt1 = __builtin_amdgcn_s_memrealtime();
 
   // iteration j, phase P = j & 1: scores of tile j are in (P ? sb : sa), the next tile's go to
   // the other array (static renaming: the loop is unrolled by two)
@@ -667,12 +673,31 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void flash_fwd_pipe_kernel(
     iter(j, std::integral_constant<int, 0>{});
     if (j + 1 < ntiles) iter(j + 1, std::integral_constant<int, 1>{});
   }
+  if (prof) pt2 = __builtin_amdgcn_s_memrealtime();
 
   l += __shfl_xor(l, 32, 64);
   const float inv = 1.f / l;
   store_row16<E, NDB>(out + ((long)b * S + min(qrow, S - 1)) * ldo + (long)h * D, hi, qrow < S,
                       [&](int db, int i) { return o[db][i] * inv; });
   if (qrow < S && hi == 0) lse2[((long)b * Hq + h) * stat_stride(S) + qrow] = m + log2f(l);
+  if (prof) {
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    if (tid == 0) {
+      unsigned hw, xcc;
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+      long long* r = prof + (long)blockIdx.x * 8;
+      r[0] = pt0;
+      r[1] = pt1;
+      r[2] = pt2;
+      r[3] = __builtin_amdgcn_s_memrealtime();
+      r[4] = hw;
+      r[5] = xcc;
+      r[6] = qt * 4;
+      r[7] = ntiles;
+    }
+  }
 }
 
 // ================================================================== backward
@@ -1611,6 +1636,14 @@ int g_fwd_split = -1;
 // S = 2048, profiles/r3_flash_fwd_pipe.log.)
 int g_fwd_pipe = 1;
 
+// Per-block timestamps of the pipelined forward (int64 [grid, 8]; flash_set_fwd_prof, for
+// scripts/flash_fwd_timeline.py); nullptr = off. (Measured with it, round 5: running the heavy
+// query tiles as two key halves merged through an agent-scope hand-off made the S = 2048 layer
+// slower, 49.2 -> 63.6 us: the extra blocks' prologue (~4-5 us of load latency each) and the
+// hand-off (epilogue 2.0 -> 6.3 us) cost more than the balance gained; at S = 8192 it balanced
+// the CUs but the span stayed 746 us. profiles/r5_flash_fwd_timeline_khalf.log.)
+long long* g_fwd_prof = nullptr;
+
 // dQ key split (see flash_bwd_dq_kernel): -1 default (on), 0 off, 1 on (flash_set_dq_split, for A/B).
 int g_dq_split = -1;
 
@@ -1705,7 +1738,7 @@ std::tuple<at::Tensor, at::Tensor> flash_fwd(const at::Tensor& qk, const at::Ten
 #define FT_FWD_PIPE(DD)                                                                            \
   hipLaunchKernelGGL((flash_fwd_pipe_kernel<E, DD, 4>), grid, block, 0, ft_stream(), cptr<bf16_t>(qk), \
                      cptr<bf16_t>(qkv), mptr<bf16_t>(out), mptr<float>(lse), B, (int)S, (int)Hq,   \
-                     (int)Hkv, sl2, ldqk)
+                     (int)Hkv, sl2, ldqk, g_fwd_prof)
   const bool pipe = !split && g_fwd_pipe >= 1;
   FT_DISPATCH_E16(qk.scalar_type(), {
     if (D == 128) {
@@ -1877,6 +1910,14 @@ void flash_set_dkdv2(bool on) { g_dkdv2 = on; }
 void flash_set_fwd_split(int64_t v) { g_fwd_split = (int)v; }
 void flash_set_dq_split(int64_t v) { g_dq_split = (int)v; }
 void flash_set_fwd_pipe(int64_t v) { g_fwd_pipe = (int)v; }
+void flash_set_fwd_prof(const std::optional<at::Tensor>& buf) {
+  if (buf.has_value()) {
+    TORCH_CHECK(buf->scalar_type() == at::kLong && buf->is_contiguous(), "flash_set_fwd_prof: int64 buffer");
+    g_fwd_prof = reinterpret_cast<long long*>(buf->data_ptr<int64_t>());
+  } else {
+    g_fwd_prof = nullptr;
+  }
+}
 void flash_set_kv_split(int64_t v) { g_kv_split = (int)v; }
 void flash_set_bwd_fold(bool on) { g_bwd_fold = on; }
 
@@ -1885,6 +1926,7 @@ TORCH_LIBRARY_FRAGMENT(ftamd, m) {
   m.def("flash_set_fwd_split(int v) -> ()", &flash_set_fwd_split);
   m.def("flash_set_dq_split(int v) -> ()", &flash_set_dq_split);
   m.def("flash_set_fwd_pipe(int v) -> ()", &flash_set_fwd_pipe);
+  m.def("flash_set_fwd_prof(Tensor? buf) -> ()", &flash_set_fwd_prof);
   m.def("flash_set_kv_split(int v) -> ()", &flash_set_kv_split);
   m.def("flash_set_bwd_fold(bool on) -> ()", &flash_set_bwd_fold);
   m.def("flash_fwd(Tensor qk, Tensor qkv, int S, int Hq, int Hkv, int D) -> (Tensor, Tensor)",

@@ -203,6 +203,7 @@ struct W4Args {
   // its own in the epilogue (fixed order: deterministic) and re-arms the flags for the next launch.
   int splits;
   int dbg;               // timing probes only (gemm_w4_set_dbg): bit 0 = skip the epilogue's global stores
+  long long* prof;       // timing probe (gemm_w4_set_prof; scripts/w4_timeline.py): [grid][8] int64
   int* tick;             // [8 * tiles] int32, zero between launches (per device and stream)
   float* ws;             // [tiles * (S - 1) * 256 * BN] fp32
 };
@@ -404,6 +405,9 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(W4Args p) {
   __shared__ __attribute__((aligned(1024))) char smem[LDS];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // timing probe: exit stamp (probe_end). (Any stamp before the drain - even one stored at entry,
+  // older than every DMA - made the compiler move address clamps into the dW K loops: the static
+  // check rejects such builds.)
   const int wm = wid >> 1, wn = wid & 1;
   constexpr int BN = 32 * NJ, NW = 16 * NJ;
   const int ntiles = p.tiles_m * p.tiles_n;
@@ -541,6 +545,22 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(W4Args p) {
   // dead LDS reads had not returned yet)
   tie_frags(f);
   tie_acc(acc);
+  auto probe_end = [&]() {
+    if (p.prof == nullptr) return;
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    if (tid == 0) {
+      unsigned hw, xcc;
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+      long long* r = p.prof + (long)blockIdx.x * 8;
+      r[3] = __builtin_amdgcn_s_memrealtime();
+      r[4] = hw;
+      r[5] = xcc;
+      r[6] = tb;
+      r[7] = nk;
+    }
+  };
 
   // (the dW layout, k-major A, has no split-K: its tile grids fill the chip, and the extra live
   // registers of the hand-off pushed its widest tile into scratch)
@@ -575,6 +595,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(W4Args p) {
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           __hip_atomic_store(flags + ks, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
+        probe_end();
         return;
       }
       if (wid == 0) {
@@ -757,7 +778,10 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(W4Args p) {
         *reinterpret_cast<uint4*>(gl + off) = av;
       }
     }
-    if (p.actT == nullptr) return;  // uniform
+    if (p.actT == nullptr) {  // uniform
+      probe_end();
+      return;
+    }
     __syncthreads();
     // a^T [F, M]: a thread takes 8 tokens x 8 features (8 row-chunk LDS reads, feature chunk
     // fastest across lanes: distinct XOR-swizzled chunks, conflict-free), transposes the block in
@@ -790,6 +814,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(W4Args p) {
       }
     }
   }
+  probe_end();
 }
 
 template <class E, int NJ, bool AT, bool BT>

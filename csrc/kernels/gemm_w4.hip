@@ -122,9 +122,11 @@ int* splitk_ticks(const c10::Device& dev, hipStream_t st, long n) {
 // workspace alive until the launch is enqueued (the caching allocator orders its reuse on the
 // stream). Falls back to one workgroup per tile where the split cannot run.
 int g_dbg = 0;  // timing probes (gemm_w4_set_dbg): W4Args::dbg of every launch
+long long* g_prof = nullptr;  // per-workgroup stamps (gemm_w4_set_prof): W4Args::prof of every launch
 
 void setup_split(W4Args& p, int splits, int nj, const at::Tensor& like, at::Tensor& ws_hold) {
   p.dbg = g_dbg;
+  p.prof = g_prof;
   p.splits = 1;
   if (splits < 2) return;
   TORCH_CHECK(splits <= 8, "gemm_w4: split-K of 2 .. 8");
@@ -169,6 +171,7 @@ at::Tensor gemm_nt_w4(const at::Tensor& a, const at::Tensor& b, const std::optio
     c = at::empty({M, N}, a.options());
   }
   W4Args p{};
+  p.prof = g_prof;
   p.a = cptr<bf16_t>(a);
   p.b = cptr<bf16_t>(b);
   p.c = mptr<bf16_t>(c);
@@ -231,6 +234,7 @@ at::Tensor gemm_w4_ex(const at::Tensor& a, bool a_t, const at::Tensor& b, bool b
     c = at::empty({M, N}, a.options());
   }
   W4Args p{};
+  p.prof = g_prof;
   p.a = cptr<bf16_t>(a);
   p.b = cptr<bf16_t>(b);
   p.c = mptr<bf16_t>(c);
@@ -282,6 +286,7 @@ at::Tensor gemm_qkv_rope_w4(const at::Tensor& x, const at::Tensor& w, const at::
   const at::DeviceGuard guard(x.device());
   auto c = at::empty({M, N}, x.options());
   W4Args p{};
+  p.prof = g_prof;
   p.a = cptr<bf16_t>(x);
   p.b = cptr<bf16_t>(w);
   p.c = mptr<bf16_t>(c);
@@ -326,6 +331,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> gemm_swiglu_w4(const at::Tensor& 
   auto a = at::empty({M, F}, x.options());
   auto aT = with_t ? at::empty({F, M}, x.options()) : at::empty({0}, x.options());
   W4Args p{};
+  p.prof = g_prof;
   p.a = cptr<bf16_t>(x);
   p.b = cptr<bf16_t>(w13);
   p.c = mptr<bf16_t>(gu);
@@ -368,6 +374,7 @@ at::Tensor gemm_swiglu_bwd_w4(const at::Tensor& dy, const at::Tensor& w2, const 
   const at::DeviceGuard guard(dy.device());
   auto dgu = at::empty({M, 2 * F}, dy.options());
   W4Args p{};
+  p.prof = g_prof;
   p.a = cptr<bf16_t>(dy);
   p.b = cptr<bf16_t>(w2);
   p.c = mptr<bf16_t>(dgu);
@@ -398,6 +405,14 @@ void gemm_w4_set_splitk(int64_t mode) { g_splitk_mode = (int)mode; }
 // timing probes only (scripts/w4_overhead_probe.py): bit 0 skips the store / residual epilogues'
 // global stores (the output is left unwritten)
 void gemm_w4_set_dbg(int64_t v) { g_dbg = (int)v; }
+void gemm_w4_set_prof(const std::optional<at::Tensor>& buf) {
+  if (buf.has_value()) {
+    TORCH_CHECK(buf->scalar_type() == at::kLong && buf->is_contiguous(), "gemm_w4_set_prof: int64 buffer");
+    g_prof = reinterpret_cast<long long*>(buf->data_ptr<int64_t>());
+  } else {
+    g_prof = nullptr;
+  }
+}
 
 // (tile width / 32, splits) the automatic choice takes for C[M, N] over a K-deep sum
 std::vector<int64_t> gemm_w4_plan(int64_t M, int64_t N, int64_t K, bool a_t, bool b_t) {
@@ -415,6 +430,7 @@ TORCH_LIBRARY_FRAGMENT(ftamd, m) {
   m.def("gemm_w4_plan(int M, int N, int K, bool a_t=False, bool b_t=False) -> int[]", &gemm_w4_plan);
   m.def("gemm_w4_set_splitk(int mode) -> ()", &gemm_w4_set_splitk);
   m.def("gemm_w4_set_dbg(int v) -> ()", &gemm_w4_set_dbg);
+  m.def("gemm_w4_set_prof(Tensor? buf) -> ()", &gemm_w4_set_prof);
   m.def("gemm_qkv_rope_w4(Tensor x, Tensor w, Tensor cos, Tensor sin, int seq, int hq, int hkv, int d) -> Tensor",
         &gemm_qkv_rope_w4);
   m.def("gemm_w4_pick(int M, int N) -> int", &gemm_w4_pick);

@@ -276,3 +276,28 @@ def test_flash_bwd_in_kernel_gqa_fold(B, S, Hq, Hkv, D, rope):
         K.flash_set_bwd_fold(False)
     for g in outs:
         assert torch.equal(g, ref)  # (G = 16 > 8: the fold is skipped, the finalize pass runs)
+
+
+def test_flash_fwd_timing_probe():
+    """flash_set_fwd_prof (scripts/flash_fwd_timeline.py): one row of ordered stamps per block, and
+    the probed forward's output equals the unprobed one."""
+    from fault_tolerant_llm_training_amd._native import kernels
+
+    K = kernels()
+    torch.manual_seed(9)
+    S, Hq, Hkv, D = 1024, 8, 2, 128
+    qkv = torch.randn(S, (Hq + 2 * Hkv) * D, device="cuda").bfloat16()
+    qk = torch.randn(S, (Hq + Hkv) * D, device="cuda").bfloat16()
+    o0, _ = K.flash_fwd(qk, qkv, S, Hq, Hkv, D)
+    buf = torch.zeros((S // 128) * Hq, 8, dtype=torch.int64, device="cuda")
+    try:
+        K.flash_set_fwd_prof(buf)
+        o1, _ = K.flash_fwd(qk, qkv, S, Hq, Hkv, D)
+        torch.cuda.synchronize()
+    finally:
+        K.flash_set_fwd_prof(None)
+    assert torch.equal(o0, o1)
+    p = buf.cpu()
+    assert (p[:, 0] > 0).all()
+    assert (p[:, 1] >= p[:, 0]).all() and (p[:, 2] >= p[:, 1]).all() and (p[:, 3] >= p[:, 2]).all()
+    assert sorted(set((p[:, 6] // 4).tolist())) == list(range(S // 128))

@@ -201,3 +201,24 @@ def test_split_k_8b_head_dx_vs_fp32():
     ref = a[rows].float() @ b.float()
     assert rel(c[rows], ref) < 4e-3
     assert torch.equal(c, K().gemm_w4_ex(a, False, b, True, M, N, Kd, None, False, None, 8, 2))
+
+
+def test_w4_timing_probe():
+    """gemm_w4_set_prof (scripts/w4_timeline.py): one exit stamp per workgroup, output unchanged."""
+    k = K()
+    torch.manual_seed(11)
+    M, N, Kd = 1024, 1024, 512
+    a = torch.randint(-2, 3, (Kd, M), device="cuda").bfloat16()
+    b = torch.randint(-2, 3, (Kd, N), device="cuda").bfloat16()
+    c0 = k.gemm_w4_ex(a, True, b, True, M, N, Kd, None, False, None, 8, 1)
+    buf = torch.zeros((M // 256) * (N // 256), 8, dtype=torch.int64, device="cuda")
+    try:
+        k.gemm_w4_set_prof(buf)
+        c1 = k.gemm_w4_ex(a, True, b, True, M, N, Kd, None, False, None, 8, 1)
+        torch.cuda.synchronize()
+    finally:
+        k.gemm_w4_set_prof(None)
+    assert torch.equal(c0, c1)
+    p = buf.cpu()
+    assert (p[:, 3] > 0).all()
+    assert sorted(p[:, 6].tolist()) == list(range(buf.shape[0]))
