@@ -185,6 +185,7 @@ struct W4Args {
   int M, N, K;
   int tiles_m, tiles_n;
   int nfast;             // raster N-fastest inside an XCD's range (A is the larger operand)
+  int group;             // > 1: grouped raster, bands of `group` slow-dimension tiles (tile_of)
   int rope_cols;         // RoPE: columns [0, rope_cols) are rotated (Hq + Hkv heads)
   int rope_hd;           // head dim
   int rope_seq;          // sequence length (position = row % seq)
@@ -209,11 +210,25 @@ struct W4Args {
 };
 
 // (tm, tn) of workgroup bid (returned by value: through references the pair went to scratch)
-__device__ __forceinline__ int2 tile_of(int bid, int tiles_m, int tiles_n, int nfast) {
+// Workgroup bid runs on XCD bid % 8 (round-robin dispatch); each XCD takes a contiguous range w of
+// the raster, so the tiles one XCD runs together share operand panels in its L2. group > 1: the
+// raster sweeps bands of `group` slow-dimension tiles (the XCD's 32 concurrent tiles then form a
+// group x 32/group block: fewer distinct panels per K-step than a 1- or 2-row strip).
+__device__ __forceinline__ int2 tile_of(int bid, int tiles_m, int tiles_n, int nfast, int group) {
   const int nwg = tiles_m * tiles_n;
   const int q = nwg / 8, rem = nwg % 8;
   const int x = bid % 8, o = bid / 8;
   const int w = (x < rem ? x * (q + 1) : rem * (q + 1) + (x - rem) * q) + o;
+  if (group > 1) {
+    if (nfast) {
+      const int band = group * tiles_n, g = w / band, r = w - g * band;
+      const int gm = min(group, tiles_m - g * group);
+      return make_int2(g * group + r % gm, r / gm);
+    }
+    const int band = group * tiles_m, g = w / band, r = w - g * band;
+    const int gn = min(group, tiles_n - g * group);
+    return make_int2(r / gn, g * group + r % gn);
+  }
   return nfast ? make_int2(w / tiles_n, w % tiles_n) : make_int2(w % tiles_m, w / tiles_m);
 }
 
@@ -407,14 +422,19 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(W4Args p) {
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   // timing probe: exit stamp (probe_end). (Any stamp before the drain - even one stored at entry,
   // older than every DMA - made the compiler move address clamps into the dW K loops: the static
-  // check rejects such builds.)
+  // check rejects such builds.) The investigation build (-DFT_W4_PROBE, scripts/w4_probe_build.py:
+  // a separate library loaded through FT_KERNELS_SO, not statically checked) also stamps the entry,
+  // the end of the prologue, the drain and the end of the epilogue's LDS staging.
+#ifdef FT_W4_PROBE
+  long long pt0 = __builtin_amdgcn_s_memrealtime(), pt1 = 0, pt2 = 0, pt3 = 0;
+#endif
   const int wm = wid >> 1, wn = wid & 1;
   constexpr int BN = 32 * NJ, NW = 16 * NJ;
   const int ntiles = p.tiles_m * p.tiles_n;
   const int nsplit = p.splits > 1 ? p.splits : 1;
   const int ks = blockIdx.x / ntiles;        // K slice of a split-K tile (0 without split)
   const int tb = blockIdx.x - ks * ntiles;   // output tile
-  const int2 tt = tile_of(tb, p.tiles_m, p.tiles_n, p.nfast);
+  const int2 tt = tile_of(tb, p.tiles_m, p.tiles_n, p.nfast, p.group);
   const int tm = tt.x, tn = tt.y;
   const int m0 = tm * BM, n0 = tn * BN;
   const int f0 = tn * NW;  // W4_SWIGLU: first feature of the tile (NW features of w1 and of w3)
@@ -511,6 +531,9 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(W4Args p) {
   sfor<NJ>([&](auto Q) { dma16<S::B_AT(1) + Q * 4 * PIECE>(c.srdB, c.voB[Q], c.stepB, sb); });
   vmcnt<S::D>();
   barrier();
+#ifdef FT_W4_PROBE
+  pt1 = __builtin_amdgcn_s_memrealtime();
+#endif
   sfor<S::R>([&](auto RR) { rd<NJ, AT, BT, 0, 0, RR>(f.a0, f.b0, c); });
 
   // the zeroed accumulators are MFMA sources next (VALU write -> MFMA SrcC wait states): the
@@ -545,6 +568,9 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(W4Args p) {
   // dead LDS reads had not returned yet)
   tie_frags(f);
   tie_acc(acc);
+#ifdef FT_W4_PROBE
+  pt2 = __builtin_amdgcn_s_memrealtime();
+#endif
   auto probe_end = [&]() {
     if (p.prof == nullptr) return;
     __builtin_amdgcn_s_waitcnt(0);
@@ -559,6 +585,12 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(W4Args p) {
       r[5] = xcc;
       r[6] = tb;
       r[7] = nk;
+#ifdef FT_W4_PROBE
+      r[0] = pt0;
+      r[1] = pt1;
+      r[2] = pt2;
+      r[7] = pt3;
+#endif
     }
   };
 
@@ -663,6 +695,9 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(W4Args p) {
   }
   __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes landed
   __builtin_amdgcn_wave_barrier();
+#ifdef FT_W4_PROBE
+  pt3 = __builtin_amdgcn_s_memrealtime();
+#endif
   const int cc = lane & 15;
   float sq = 0.f;  // sum of squares of the stored values (p.part)
   if constexpr (EPI == W4_SWIGLU_BWD) {

@@ -123,6 +123,7 @@ int* splitk_ticks(const c10::Device& dev, hipStream_t st, long n) {
 // stream). Falls back to one workgroup per tile where the split cannot run.
 int g_dbg = 0;  // timing probes (gemm_w4_set_dbg): W4Args::dbg of every launch
 long long* g_prof = nullptr;  // per-workgroup stamps (gemm_w4_set_prof): W4Args::prof of every launch
+int g_group = 0;              // grouped tile raster (gemm_w4_set_group): W4Args::group of every launch
 
 void setup_split(W4Args& p, int splits, int nj, const at::Tensor& like, at::Tensor& ws_hold) {
   p.dbg = g_dbg;
@@ -172,6 +173,7 @@ at::Tensor gemm_nt_w4(const at::Tensor& a, const at::Tensor& b, const std::optio
   }
   W4Args p{};
   p.prof = g_prof;
+  p.group = g_group;
   p.a = cptr<bf16_t>(a);
   p.b = cptr<bf16_t>(b);
   p.c = mptr<bf16_t>(c);
@@ -235,6 +237,7 @@ at::Tensor gemm_w4_ex(const at::Tensor& a, bool a_t, const at::Tensor& b, bool b
   }
   W4Args p{};
   p.prof = g_prof;
+  p.group = g_group;
   p.a = cptr<bf16_t>(a);
   p.b = cptr<bf16_t>(b);
   p.c = mptr<bf16_t>(c);
@@ -287,6 +290,7 @@ at::Tensor gemm_qkv_rope_w4(const at::Tensor& x, const at::Tensor& w, const at::
   auto c = at::empty({M, N}, x.options());
   W4Args p{};
   p.prof = g_prof;
+  p.group = g_group;
   p.a = cptr<bf16_t>(x);
   p.b = cptr<bf16_t>(w);
   p.c = mptr<bf16_t>(c);
@@ -332,6 +336,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> gemm_swiglu_w4(const at::Tensor& 
   auto aT = with_t ? at::empty({F, M}, x.options()) : at::empty({0}, x.options());
   W4Args p{};
   p.prof = g_prof;
+  p.group = g_group;
   p.a = cptr<bf16_t>(x);
   p.b = cptr<bf16_t>(w13);
   p.c = mptr<bf16_t>(gu);
@@ -375,6 +380,7 @@ at::Tensor gemm_swiglu_bwd_w4(const at::Tensor& dy, const at::Tensor& w2, const 
   auto dgu = at::empty({M, 2 * F}, dy.options());
   W4Args p{};
   p.prof = g_prof;
+  p.group = g_group;
   p.a = cptr<bf16_t>(dy);
   p.b = cptr<bf16_t>(w2);
   p.c = mptr<bf16_t>(dgu);
@@ -405,6 +411,7 @@ void gemm_w4_set_splitk(int64_t mode) { g_splitk_mode = (int)mode; }
 // timing probes only (scripts/w4_overhead_probe.py): bit 0 skips the store / residual epilogues'
 // global stores (the output is left unwritten)
 void gemm_w4_set_dbg(int64_t v) { g_dbg = (int)v; }
+void gemm_w4_set_group(int64_t v) { g_group = (int)v; }
 void gemm_w4_set_prof(const std::optional<at::Tensor>& buf) {
   if (buf.has_value()) {
     TORCH_CHECK(buf->scalar_type() == at::kLong && buf->is_contiguous(), "gemm_w4_set_prof: int64 buffer");
@@ -430,6 +437,7 @@ TORCH_LIBRARY_FRAGMENT(ftamd, m) {
   m.def("gemm_w4_plan(int M, int N, int K, bool a_t=False, bool b_t=False) -> int[]", &gemm_w4_plan);
   m.def("gemm_w4_set_splitk(int mode) -> ()", &gemm_w4_set_splitk);
   m.def("gemm_w4_set_dbg(int v) -> ()", &gemm_w4_set_dbg);
+  m.def("gemm_w4_set_group(int v) -> ()", &gemm_w4_set_group);
   m.def("gemm_w4_set_prof(Tensor? buf) -> ()", &gemm_w4_set_prof);
   m.def("gemm_qkv_rope_w4(Tensor x, Tensor w, Tensor cos, Tensor sin, int seq, int hq, int hkv, int d) -> Tensor",
         &gemm_qkv_rope_w4);

@@ -7,6 +7,11 @@ Only the exit is stamped: any stamp before the K loop's drain changed the dW loo
 (csrc/kernels/gemm_w4.h, probe_end).
 
     python scripts/w4_timeline.py
+    FT_KERNELS_SO=probe/_kernels_probe.so python scripts/w4_timeline.py --full   (scripts/w4_probe_build.py)
+
+--full: the investigation build also stamps the entry, the end of the prologue, the drain and the
+end of the epilogue's LDS staging: prints the per-workgroup phase split and the gap between one
+workgroup's exit and the next one's entry on the same CU.
 """
 import os
 import sys
@@ -34,6 +39,23 @@ def timeit(fn, n=10, w=3):
     return s.elapsed_time(e) / n * 1e3
 
 
+FULL = "--full" in sys.argv
+
+
+def phases(p):
+    t0, t1, t2, t3, t7 = (p[:, i].astype(np.int64) for i in (0, 1, 2, 3, 7))
+    pro, loop, stage, epi = (t1 - t0) / 100, (t2 - t1) / 100, (t7 - t2) / 100, (t3 - t7) / 100
+    cu = (p[:, 5] << 16) | ((p[:, 4] >> 8) & 0xFF)
+    gaps = []
+    for c in set(cu.tolist()):
+        m = cu == c
+        iv = sorted(zip(t0[m].tolist(), t3[m].tolist()))
+        gaps += [(b0 - a1) / 100 for (_, a1), (b0, _) in zip(iv, iv[1:])]
+    f = lambda x: f"{np.mean(x):6.2f} (p10 {np.percentile(x, 10):6.2f} p90 {np.percentile(x, 90):6.2f})"  # noqa: E731
+    print(f"    prologue {f(pro)} | K loop {f(loop)} | epilogue staging {f(stage)} | rest of epilogue {f(epi)} us"
+          + (f" | exit -> next entry on the CU {f(gaps)} us" if gaps else ""), flush=True)
+
+
 def probe(name, fn, grid):
     t_us = timeit(fn)
     buf = torch.zeros(grid, 8, dtype=torch.int64, device="cuda")
@@ -43,6 +65,9 @@ def probe(name, fn, grid):
     K_.gemm_w4_set_prof(None)
     p = buf.cpu().numpy()
     p = p[p[:, 3] != 0]
+    if FULL:
+        print(name, flush=True)
+        phases(p)
     end = (p[:, 3] - p[:, 3].min()) / 100.0  # us after the first exit
     cu = (p[:, 5] << 16) | ((p[:, 4] >> 8) & 0xFF) | (((p[:, 4] >> 13) & 0x7) << 8)
     per_cu = {}

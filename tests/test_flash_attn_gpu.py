@@ -288,14 +288,16 @@ def test_flash_fwd_timing_probe():
     S, Hq, Hkv, D = 1024, 8, 2, 128
     qkv = torch.randn(S, (Hq + 2 * Hkv) * D, device="cuda").bfloat16()
     qk = torch.randn(S, (Hq + Hkv) * D, device="cuda").bfloat16()
-    o0, _ = K.flash_fwd(qk, qkv, S, Hq, Hkv, D)
     buf = torch.zeros((S // 128) * Hq, 8, dtype=torch.int64, device="cuda")
     try:
+        K.flash_set_fwd_split(0)  # the probe is in the pipelined (unsplit) kernel
+        o0, _ = K.flash_fwd(qk, qkv, S, Hq, Hkv, D)
         K.flash_set_fwd_prof(buf)
         o1, _ = K.flash_fwd(qk, qkv, S, Hq, Hkv, D)
         torch.cuda.synchronize()
     finally:
         K.flash_set_fwd_prof(None)
+        K.flash_set_fwd_split(-1)
     assert torch.equal(o0, o1)
     p = buf.cpu()
     assert (p[:, 0] > 0).all()

@@ -222,3 +222,36 @@ def test_w4_timing_probe():
     p = buf.cpu()
     assert (p[:, 3] > 0).all()
     assert sorted(p[:, 6].tolist()) == list(range(buf.shape[0]))
+
+
+@pytest.mark.parametrize("group", [2, 3, 4, 8])
+def test_w4_grouped_raster_bitwise(group):
+    """gemm_w4_set_group: a different tile -> workgroup order only; every layout, split-K and the
+    sum-of-squares partials are bitwise the default raster's (incl. a last band shorter than G)."""
+    k = K()
+    torch.manual_seed(13)
+    cases = []
+    a, b = rnd(2048, 1024), rnd(1792, 1024)  # fwd: 8 x 14 tiles at NJ 4
+    cases.append(lambda: (k.gemm_nt_w4(a, b, None, None),))
+    a2, b2 = rnd(1280, 4096), rnd(4096, 1024)  # dX, split-K picked by the plan
+    cases.append(lambda: (k.gemm_w4_ex(a2, False, b2, True, 1280, 1024, 4096, None, False, None, 0),))
+    a3, b3 = rnd(512, 2816), rnd(512, 768)  # dW with partials: 11 x 3 tiles (M > N: n fastest)
+    part = torch.zeros(11 * 6, device="cuda")
+
+    def dw():
+        part.zero_()
+        c = k.gemm_w4_ex(a3, True, b3, True, 2816, 768, 512, None, False, part, 0)
+        return c, part.clone()
+
+    cases.append(dw)
+    x, w13 = rnd(1024, 512), rnd(2 * 896, 512)
+    cases.append(lambda: k.gemm_swiglu_w4(x, w13, True))
+    ref = [f() for f in cases]
+    try:
+        k.gemm_w4_set_group(group)
+        got = [f() for f in cases]
+    finally:
+        k.gemm_w4_set_group(0)
+    for r_, g_ in zip(ref, got):
+        for u, v in zip(r_, g_):
+            assert torch.equal(u, v)
