@@ -123,7 +123,13 @@ int* splitk_ticks(const c10::Device& dev, hipStream_t st, long n) {
 // stream). Falls back to one workgroup per tile where the split cannot run.
 int g_dbg = 0;  // timing probes (gemm_w4_set_dbg): W4Args::dbg of every launch
 long long* g_prof = nullptr;  // per-workgroup stamps (gemm_w4_set_prof): W4Args::prof of every launch
-int g_group = 0;              // grouped tile raster (gemm_w4_set_group): W4Args::group of every launch
+// Grouped tile raster (W4Args::group, tile_of): the XCD's 32 concurrent tiles as a G x 32/G block.
+// -1 (default): 8 for the dW layout (k-major A), 4 otherwise; >= 0 forces (0: the plain raster).
+// Measured per 8B product (scripts/w4_raster_bench.py, profiles/r5_w4_raster_sweep2.log): w13 dW
+// 392 -> 348 us, head dW 1823 -> 1682, head dX 1498 -> 1442, w2 / w13 forward 1.02x; the small
+// one-round products unchanged.
+int g_group = -1;
+int raster_group(bool a_t) { return g_group >= 0 ? g_group : (a_t ? 8 : 4); }
 
 void setup_split(W4Args& p, int splits, int nj, const at::Tensor& like, at::Tensor& ws_hold) {
   p.dbg = g_dbg;
@@ -173,7 +179,7 @@ at::Tensor gemm_nt_w4(const at::Tensor& a, const at::Tensor& b, const std::optio
   }
   W4Args p{};
   p.prof = g_prof;
-  p.group = g_group;
+  p.group = raster_group(false);
   p.a = cptr<bf16_t>(a);
   p.b = cptr<bf16_t>(b);
   p.c = mptr<bf16_t>(c);
@@ -237,7 +243,7 @@ at::Tensor gemm_w4_ex(const at::Tensor& a, bool a_t, const at::Tensor& b, bool b
   }
   W4Args p{};
   p.prof = g_prof;
-  p.group = g_group;
+  p.group = raster_group(false);
   p.a = cptr<bf16_t>(a);
   p.b = cptr<bf16_t>(b);
   p.c = mptr<bf16_t>(c);
@@ -252,6 +258,7 @@ at::Tensor gemm_w4_ex(const at::Tensor& a, bool a_t, const at::Tensor& b, bool b
   p.tiles_m = M / BM;
   p.tiles_n = N / (32 * NJ);
   p.nfast = M > N;  // keep the larger operand's panels inside one XCD
+  p.group = raster_group(a_t);
   if (part.has_value() && part->defined()) {
     FT_CHECK_F32((*part));
     FT_CHECK_CONTIG((*part));
@@ -290,7 +297,7 @@ at::Tensor gemm_qkv_rope_w4(const at::Tensor& x, const at::Tensor& w, const at::
   auto c = at::empty({M, N}, x.options());
   W4Args p{};
   p.prof = g_prof;
-  p.group = g_group;
+  p.group = raster_group(false);
   p.a = cptr<bf16_t>(x);
   p.b = cptr<bf16_t>(w);
   p.c = mptr<bf16_t>(c);
@@ -336,7 +343,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> gemm_swiglu_w4(const at::Tensor& 
   auto aT = with_t ? at::empty({F, M}, x.options()) : at::empty({0}, x.options());
   W4Args p{};
   p.prof = g_prof;
-  p.group = g_group;
+  p.group = raster_group(false);
   p.a = cptr<bf16_t>(x);
   p.b = cptr<bf16_t>(w13);
   p.c = mptr<bf16_t>(gu);
@@ -380,7 +387,7 @@ at::Tensor gemm_swiglu_bwd_w4(const at::Tensor& dy, const at::Tensor& w2, const 
   auto dgu = at::empty({M, 2 * F}, dy.options());
   W4Args p{};
   p.prof = g_prof;
-  p.group = g_group;
+  p.group = raster_group(false);
   p.a = cptr<bf16_t>(dy);
   p.b = cptr<bf16_t>(w2);
   p.c = mptr<bf16_t>(dgu);

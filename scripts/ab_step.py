@@ -112,7 +112,8 @@ def main():
                "psums": lambda on: (torch.cuda.synchronize(), red.set_producer_sums(on)),
                "splitk": lambda on: (torch.cuda.synchronize(), Fx.set_w4_splitk(1 if on else 0)),
                "w4dwside": lambda on: (torch.cuda.synchronize(), setattr(Fx, "_W4_DW_SIDE", on)),
-               "gemm_s": lambda on: (torch.cuda.synchronize(), Fx.set_gemm_s(on))}
+               "gemm_s": lambda on: (torch.cuda.synchronize(), Fx.set_gemm_s(on)),
+               "raster": lambda on: (torch.cuda.synchronize(), kernels().gemm_w4_set_group(-1 if on else 0))}
     configs = list(itertools.product([False, True], repeat=len(knobs)))
 
     def apply(cfg):

@@ -66,7 +66,7 @@ def main():
             for g in groups:
                 K_.gemm_w4_set_group(g)
                 best[g] = min(best[g], timeit(fn))
-        K_.gemm_w4_set_group(0)
+        K_.gemm_w4_set_group(-1)
         for g in groups:
             tot[g] += best[g]
         b0 = best[groups[0]]

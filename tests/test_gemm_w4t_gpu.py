@@ -251,7 +251,7 @@ def test_w4_grouped_raster_bitwise(group):
         k.gemm_w4_set_group(group)
         got = [f() for f in cases]
     finally:
-        k.gemm_w4_set_group(0)
+        k.gemm_w4_set_group(-1)
     for r_, g_ in zip(ref, got):
         for u, v in zip(r_, g_):
             assert torch.equal(u, v)
