@@ -52,6 +52,7 @@ _W4_DTYPES = (torch.bfloat16, torch.float16)  # bf16 / fp16 MFMA variants of the
 # Workgroups (output tiles x K slices) a product needs before it goes to the w4 kernel: half the
 # chip. (Tests lower it to drive small shapes through the same paths.)
 _W4_MIN_TILES = 128
+_W4_SHORT_K = 1024
 
 
 def set_w4_fwd(on: bool) -> None:
@@ -85,7 +86,13 @@ def w4_route(M: int, N: int, K: int, a_t: bool, b_t: bool, *ts) -> bool:
     if M % 256 or K % 128 or K < 128:  # K-tiles of 64 in pairs
         return False
     nj, splits = _w4_plan(M, N, K, a_t, b_t)
-    return nj > 0 and (M // 256) * (N // (32 * nj)) * splits >= _W4_MIN_TILES
+    if nj == 0:
+        return False
+    wgs = (M // 256) * (N // (32 * nj)) * splits
+    # short reductions (K <= 1024, the GPT-2 wo forward / dX: 48-64 tiles) beat hipBLASLt on
+    # far fewer than 256 workgroups: 14.2 vs 19.9 us (wo fwd) and 14.2 vs 18.5 us (wo dX) at
+    # GPT-2-small, 17.0 vs 19.7 / 16.8 vs 19.6 us at -medium (profiles/r5_gpt2_gemm_probe.log)
+    return wgs >= _W4_MIN_TILES or (K <= _W4_SHORT_K and not a_t and wgs >= 32)
 
 
 # GPT-2-sized forward products on the 128 x 128-tile kernel (csrc/kernels/gemm_s.hip): K <= 1024

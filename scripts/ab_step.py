@@ -71,6 +71,7 @@ def main():
     data = SyntheticTokens(a.vocab_size, a.seq_len, seed=4321)
     inv = torch.full((1,), 1.0 / a.seq_len, dtype=torch.float32, device=dev)
     it = [0]
+    serial_adamw = [False]
 
     def step():
         tok, lab = data.batch(it[0], 1)
@@ -80,6 +81,8 @@ def main():
         red.finish()
         opt.clip_grad_norm_(1.0)
         opt.step()
+        if serial_adamw[0]:  # the next forward starts after the whole optimizer step
+            opt.gate.wait_all()
         sched.step()
         return loss
 
@@ -113,6 +116,7 @@ def main():
                "splitk": lambda on: (torch.cuda.synchronize(), Fx.set_w4_splitk(1 if on else 0)),
                "w4dwside": lambda on: (torch.cuda.synchronize(), setattr(Fx, "_W4_DW_SIDE", on)),
                "gemm_s": lambda on: (torch.cuda.synchronize(), Fx.set_gemm_s(on)),
+               "adamw_serial": lambda on: serial_adamw.__setitem__(0, bool(on)),
                "raster": lambda on: (torch.cuda.synchronize(), kernels().gemm_w4_set_group(-1 if on else 0))}
     configs = list(itertools.product([False, True], repeat=len(knobs)))
 
