@@ -1,4 +1,4 @@
-"""GEMM routing table per preset and dtype (ops/functional.py: routing_table evaluates the same
+"""GEMM routing table per preset and dtype (ops/routing.py: routing_table evaluates the same
 predicates the autograd functions use, on shape/dtype specs: no GPU needed). Pins which kernel
 each product of the step takes, so a routing change is a visible test change:
 
@@ -13,6 +13,7 @@ import torch
 
 from fault_tolerant_llm_training_amd.models.llama import model_args_for
 from fault_tolerant_llm_training_amd.ops import functional as Fx
+from fault_tolerant_llm_training_amd.ops.routing import routing_table
 
 PRODUCTS = ["qkv fwd", "qkv dX", "qkv dW", "wo fwd", "wo dX", "wo dW", "w13 fwd", "w2 dX", "w13 dX", "w13 dW",
             "w2 fwd", "w2 dW", "head fwd", "head dX", "head dW"]
@@ -20,7 +21,7 @@ PRODUCTS = ["qkv fwd", "qkv dX", "qkv dW", "wo fwd", "wo dX", "wo dW", "w13 fwd"
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 def test_llama8b_every_product_on_w4(dtype):
-    t = Fx.routing_table(model_args_for("llama3-8b", vocab_size=131072, seq_len=2048), dtype)
+    t = routing_table(model_args_for("llama3-8b", vocab_size=131072, seq_len=2048), dtype)
     assert sorted(t) == sorted(PRODUCTS)
     assert t == {
         "qkv fwd": "w4 qkv+rope", "qkv dX": "w4 256 x2", "qkv dW": "w4 256",
@@ -34,14 +35,14 @@ def test_llama8b_every_product_on_w4(dtype):
 @pytest.mark.parametrize("preset", ["llama3-8b", "gpt2-small", "gpt2-medium"])
 def test_fp32_and_cpu_take_no_mfma_gemm(preset):
     a = model_args_for(preset, vocab_size=50304 if preset != "llama3-8b" else 131072, seq_len=2048)
-    assert set(Fx.routing_table(a, torch.float32).values()) == {"hipBLASLt"}
-    assert set(Fx.routing_table(a, torch.bfloat16, cuda=False).values()) == {"hipBLASLt"}
+    assert set(routing_table(a, torch.float32).values()) == {"hipBLASLt"}
+    assert set(routing_table(a, torch.bfloat16, cuda=False).values()) == {"hipBLASLt"}
 
 
 @pytest.mark.parametrize("preset,vocab", [("gpt2-small", 50304), ("gpt2-small", 131072),
                                           ("gpt2-medium", 50304), ("gpt2-medium", 131072)])
 def test_gpt2_routes(preset, vocab):
-    t = Fx.routing_table(model_args_for(preset, vocab_size=vocab, seq_len=2048), torch.bfloat16)
+    t = routing_table(model_args_for(preset, vocab_size=vocab, seq_len=2048), torch.bfloat16)
     on_w4 = sorted(k for k, v in t.items() if v.startswith("w4"))
     # the LM-head dX (K = V) always takes a K split on w4; the 768 / 1024-wide projections'
     # forward / dX with enough tiles do too; wo (2048 x D x D, K = D <= 1024) runs its 48-64 tiles
@@ -59,6 +60,6 @@ def test_blas_only_knob(monkeypatch):
     monkeypatch.setattr(Fx, "_BLAS_ONLY", True)
     from fault_tolerant_llm_training_amd.ops import attention as A
 
-    t = Fx.routing_table(model_args_for("llama3-8b", vocab_size=131072, seq_len=2048), torch.bfloat16)
+    t = routing_table(model_args_for("llama3-8b", vocab_size=131072, seq_len=2048), torch.bfloat16)
     assert set(t.values()) == {"hipBLASLt"}
     assert A._qkv_rope_ok is not None
