@@ -53,6 +53,7 @@ _W4_DTYPES = (torch.bfloat16, torch.float16)  # bf16 / fp16 MFMA variants of the
 # chip. (Tests lower it to drive small shapes through the same paths.)
 _W4_MIN_TILES = 128
 _W4_SHORT_K = 1024
+_W4_DEEP_K = 4096
 
 
 def set_w4_fwd(on: bool) -> None:
@@ -89,10 +90,13 @@ def w4_route(M: int, N: int, K: int, a_t: bool, b_t: bool, *ts) -> bool:
     if nj == 0:
         return False
     wgs = (M // 256) * (N // (32 * nj)) * splits
-    # short reductions (K <= 1024, the GPT-2 wo forward / dX: 48-64 tiles) beat hipBLASLt on
-    # far fewer than 256 workgroups: 14.2 vs 19.9 us (wo fwd) and 14.2 vs 18.5 us (wo dX) at
-    # GPT-2-small, 17.0 vs 19.7 / 16.8 vs 19.6 us at -medium (profiles/r5_gpt2_gemm_probe.log)
-    return wgs >= _W4_MIN_TILES or (K <= _W4_SHORT_K and not a_t and wgs >= 32)
+    if a_t:  # dW: no split on this layout
+        return wgs >= _W4_MIN_TILES
+    # forward / dX below a full round (GPT-2 sizes, profiles/r5_gpt2_gemm_probe.log): short
+    # reductions (K <= 1024: wo forward / dX on 48-64 tiles, 1.15-1.39x hipBLASLt) and deep
+    # split ones (K >= 4096: w1|w3 dX, 1.14-1.25x) win; the 2048-3072-deep ones in between lose
+    # (w2 forward 0.82-0.88x, -medium qkv dX 0.94x)
+    return wgs >= 256 or (K <= _W4_SHORT_K and wgs >= 32) or (K >= _W4_DEEP_K and wgs >= _W4_MIN_TILES)
 
 
 # GPT-2-sized forward products on the 128 x 128-tile kernel (csrc/kernels/gemm_s.hip): K <= 1024
@@ -121,6 +125,15 @@ def _s_ok(x2: torch.Tensor, w: torch.Tensor) -> bool:
 _W4_WIDE_MIN_K = 2048
 
 
+def _w4_fwd_ok(T: int, N: int, K: int, x2, w) -> bool:
+    """The forward product on w4; the 256-wide tile below K = 2048 only within one round (the
+    GPT-2-medium w1|w3: 176 tiles, 27.7 vs 35.0 us for hipBLASLt)."""
+    if not (_W4_FWD and w.is_contiguous() and w4_route(T, N, K, False, False, x2, w)):
+        return False
+    nj, sp = _w4_plan(T, N, K, False, False)
+    return K >= _W4_WIDE_MIN_K or nj <= 6 or (T // 256) * (N // (32 * nj)) * sp <= 256
+
+
 def mm_fwd(x2: torch.Tensor, w: torch.Tensor, residual: Optional[torch.Tensor] = None) -> torch.Tensor:
     """y = x2 @ w^T (+ residual, in the epilogue): x2 [T, K], w [N, K] (nn.Linear layout)."""
     T, K = x2.shape
@@ -128,8 +141,7 @@ def mm_fwd(x2: torch.Tensor, w: torch.Tensor, residual: Optional[torch.Tensor] =
     res = None if residual is None else residual.reshape(T, N).contiguous()
     if _s_ok(x2, w):
         return kernels().gemm_nt_s(x2.contiguous(), w, None, res, 1)
-    if _W4_FWD and w.is_contiguous() and w4_route(T, N, K, False, False, x2, w) and \
-            (K >= _W4_WIDE_MIN_K or _w4_plan(T, N, K, False, False)[0] <= 6):
+    if _w4_fwd_ok(T, N, K, x2, w):
         return kernels().gemm_nt_w4(x2.contiguous(), w, None, res, 0, 0)
     if residual is None:
         return torch.mm(x2, w.t())

@@ -37,7 +37,7 @@ def routing_table(margs, dtype, tokens: int = 2048, cuda: bool = True) -> dict:
         N = w.shape[0]
         if Fx._s_ok(xx, w):
             return "gemm_s"
-        if Fx._W4_FWD and Fx.w4_route(Tn, N, K, False, False, xx, w) and (K >= Fx._W4_WIDE_MIN_K or Fx._w4_plan(Tn, N, K, False, False)[0] <= 6):
+        if Fx._w4_fwd_ok(Tn, N, K, xx, w):
             return _w4_name(Tn, N, K, False, False)
         return "hipBLASLt"
 

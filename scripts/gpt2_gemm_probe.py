@@ -31,24 +31,33 @@ def main():
     T = 2048
     r = lambda *s: (torch.rand(*s, device="cuda") * 2 - 1).bfloat16()  # noqa: E731
     # (name, layout, M, N, K)
-    prods = [("wo fwd", "fwd", T, D, D), ("w2 fwd", "fwd", T, D, F), ("qkv dX", "dx", T, D, W),
-             ("wo dX", "dx", T, D, D), ("w13 dX", "dx", T, D, 2 * F)]
+    prods = [("wo fwd", "fwd", T, D, D), ("w2 fwd", "fwd", T, D, F), ("w13 fwd", "fwd", T, 2 * F, D),
+             ("qkv dX", "dx", T, D, W), ("wo dX", "dx", T, D, D), ("w13 dX", "dx", T, D, 2 * F),
+             ("qkv dW", "dw", W, D, T), ("wo dW", "dw", D, D, T), ("w13 dW", "dw", 2 * F, D, T),
+             ("w2 dW", "dw", D, F, T)]
     for name, lay, M, N, Kd in prods:
         if lay == "fwd":
             a, b = r(M, Kd), r(N, Kd)
             blas = lambda: torch.mm(a, b.t())  # noqa: E731
             w4 = lambda nj, sp: K_.gemm_nt_w4(a, b, None, None, nj, sp)  # noqa: E731
-        else:
+        elif lay == "dx":
             a, b = r(M, Kd), r(Kd, N)
             blas = lambda: torch.mm(a, b)  # noqa: E731
             w4 = lambda nj, sp: K_.gemm_w4_ex(a, False, b, True, M, N, Kd, None, False, None, nj, sp)  # noqa: E731
+        else:  # dW = dY^T X, both operands k-major as stored (no split-K on this layout)
+            a, b = r(Kd, M), r(Kd, N)
+            blas = lambda: torch.mm(a.t(), b)  # noqa: E731
+            w4 = lambda nj, sp: K_.gemm_w4_ex(a, True, b, True, M, N, Kd, None, False, None, nj, sp)  # noqa: E731
         tb = timeit(blas)
         cells = []
-        for nj in (4, 6):
+        if M % 256:
+            print(f"{name:8s} {M}x{N}x{Kd}: hipBLASLt {tb:6.1f} us | M % 256 != 0: no w4 tile", flush=True)
+            continue
+        for nj in (4, 6, 8):
             if N % (32 * nj):
                 continue
             tiles = (M // 256) * (N // (32 * nj))
-            for sp in (1, 2, 3, 4, 6, 8):
+            for sp in ((1,) if lay == "dw" else (1, 2, 3, 4, 6, 8)):
                 if Kd // 128 < sp or tiles * sp > 512:
                     continue
                 cells.append((timeit(lambda: w4(nj, sp)), nj, sp, tiles * sp))

@@ -84,6 +84,8 @@ def test_weight_grad_on_w4(T, N, Kd, monkeypatch):
     from fault_tolerant_llm_training_amd.ops.grad_sink import GradSink
 
     monkeypatch.setattr(Fx, "_W4_MIN_TILES", 1)
+
+    monkeypatch.setattr(Fx, "_W4_DEEP_K", 0)
     torch.manual_seed(T + N)
     dy = rnd(T, N)
     x = rnd(T, Kd)

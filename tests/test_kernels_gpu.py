@@ -257,6 +257,7 @@ def test_dw_side_stream_bitwise(w4, monkeypatch):
 
     if w4:
         monkeypatch.setattr(Fx, "_W4_MIN_TILES", 1)
+        monkeypatch.setattr(Fx, "_W4_DEEP_K", 0)
         monkeypatch.setattr(Fx, "_W4_DW_SIDE", True)
     a = model_args_for("tiny", vocab_size=1024, seq_len=256)
     tok = torch.randint(0, 1024, (2, 256), device="cuda")
@@ -343,6 +344,7 @@ def test_feed_forward_fused(w4, monkeypatch):
 
     if w4:
         monkeypatch.setattr(Fx, "_W4_MIN_TILES", 1)
+        monkeypatch.setattr(Fx, "_W4_DEEP_K", 0)
     torch.manual_seed(5)
     T, D, Fh = 256, 256, 896  # F % 112 (SwiGLU tile), 2F % 256 (dW13 rows)
     x = torch.randn(T, D, device="cuda").bfloat16().requires_grad_(True)

@@ -2,7 +2,7 @@
 
 The w4 routing only takes products with at least half the chip in output tiles (and the fused
 QKV + RoPE projection only from model dim 2048), so the tiny / GPT-2 GPU tests never reach it.
-Here those gates are lowered (``_W4_MIN_TILES``, ``_QKV_ROPE_MIN_K``) and a Llama-style model
+Here those gates are lowered (``_W4_MIN_TILES``, ``_W4_DEEP_K``, ``_QKV_ROPE_MIN_K``) and a Llama-style model
 whose FFN width is a multiple of 112 (the SwiGLU-epilogue tile) runs:
   forward  QKV GEMM with the RoPE epilogue, wo / w2 with the residual epilogue, w1|w3 with the
            SwiGLU epilogue, the LM head on the w4 kernel
@@ -28,6 +28,8 @@ def gates(monkeypatch):
     from fault_tolerant_llm_training_amd.ops import functional as Fx
 
     monkeypatch.setattr(Fx, "_W4_MIN_TILES", 1)
+
+    monkeypatch.setattr(Fx, "_W4_DEEP_K", 0)
     from fault_tolerant_llm_training_amd.ops import attention as A
 
     monkeypatch.setattr(A, "_QKV_ROPE_MIN_K", 0)
