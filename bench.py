@@ -294,7 +294,7 @@ def main():
         # board power / shader clock over the timed region (rank 0's GPU): they tell a hotter or
         # lower-clocked box from slower code. (No clock-normalised step time: across boxes the step
         # moved 0.55-0.65 % per 1 % of sclk, not 1:1 -- AdamW and the epilogues are memory-bound --
-        # docs/PERFORMANCE.md "Box-to-box variance"; compare code on one box: scripts/so_ab.sh.)
+        # docs/PERFORMANCE.md "Clock and step time"; compare code on one box: scripts/ab_step.py.)
         out.update(sampler.summary())
     if a.dp_reduce_dtype == "fp32":
         out["dp_reduce_dtype"] = "fp32"
