@@ -60,7 +60,6 @@ def flash_attn_bwd(do, qk, qkv, o, lse, S, hq, hkv, d, cos=None, sin=None):
 # --------------------------------------------------------------------------------------
 # RoPE + causal GQA attention on the fused QKV projection (autograd)
 # --------------------------------------------------------------------------------------
-from . import functional as Fx  # noqa: E402  (functional re-exports this module's names at its end)
 
 
 def rope_reference(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor) -> torch.Tensor:
@@ -219,3 +218,8 @@ def qkv_rope_attention(xn, wqkv, sink, cos, sin, seq_len, hq, hkv, d, keep: Opti
         return rope_attention(qkv, cos, sin, seq_len, hq, hkv, d, keep, gen, rotated=True)
     qkv = Fx.linear(xn, wqkv, sink)
     return rope_attention(qkv.view(-1, qkv.shape[-1]), cos, sin, seq_len, hq, hkv, d, keep, gen)
+
+
+# functional.py re-exports this module's names at its end and this module calls into functional at
+# run time: imported last, so either module can be imported first
+from . import functional as Fx  # noqa: E402
