@@ -34,9 +34,8 @@ __global__ __launch_bounds__(256) void norm_fwd_kernel(const typename E::T* __re
                                                        float* __restrict__ mean_out, int M,
                                                        int N, float eps) {
   const int lane = threadIdx.x & 63;
-  // rows in a grid stride: a capped grid (set_norm_fwd_blocks) needs fewer workgroup dispatches
-  for (int row = blockIdx.x * ROWS_PER_BLOCK + (threadIdx.x >> 6); row < M;
-       row += gridDim.x * ROWS_PER_BLOCK) {
+  const int row = blockIdx.x * ROWS_PER_BLOCK + (threadIdx.x >> 6);
+  if (row >= M) return;
   using T = typename E::T;
   const T* xr = x + (size_t)row * N;
   float v[CH][8];
@@ -93,7 +92,6 @@ __global__ __launch_bounds__(256) void norm_fwd_kernel(const typename E::T* __re
   if (lane == 0) {
     rstd[row] = r;
     if (LN) mean_out[row] = mu;
-  }
   }
 }
 
@@ -409,16 +407,12 @@ __global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ p
   }
 }
 
-int g_norm_fwd_blocks = 0;  // grid cap of the forward (0: one block per 4 rows)
-
 template <class E, bool LN, bool ADD>
 void launch_fwd(const typename E::T* x, const typename E::T* d, typename E::T* hout,
                 const typename E::T* w, typename E::T* y, float* rstd, float* mean, int M, int N,
                 float eps, hipStream_t st) {
   const int chunks = (N + 511) / 512;
-  int nb = (M + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK;
-  if (g_norm_fwd_blocks > 0) nb = std::min(nb, g_norm_fwd_blocks);
-  dim3 grid(nb), block(256);
+  dim3 grid((M + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK), block(256);
 #define FT_NF(C)                                                                             \
   hipLaunchKernelGGL((norm_fwd_kernel<E, C, LN, ADD>), grid, block, 0, st, x, d, hout, w, y, rstd, \
                      mean, M, N, eps)
@@ -643,10 +637,7 @@ at::Tensor norm_bwd(const at::Tensor& dy, const at::Tensor& x, const at::Tensor&
   return std::get<0>(r);
 }
 
-void set_norm_fwd_blocks(int64_t n) { g_norm_fwd_blocks = (int)n; }
-
 TORCH_LIBRARY_FRAGMENT(ftamd, m) {
-  m.def("set_norm_fwd_blocks(int n) -> ()", &set_norm_fwd_blocks);
   m.def("norm_fwd(Tensor x, Tensor w, float eps, bool layernorm) -> (Tensor, Tensor, Tensor)",
         &norm_fwd);
   m.def(

@@ -116,8 +116,6 @@ def main():
                "splitk": lambda on: (torch.cuda.synchronize(), Fx.set_w4_splitk(1 if on else 0)),
                "w4dwside": lambda on: (torch.cuda.synchronize(), setattr(Fx, "_W4_DW_SIDE", on)),
                "gemm_s": lambda on: (torch.cuda.synchronize(), Fx.set_gemm_s(on)),
-               "normgrid": lambda on: (torch.cuda.synchronize(), kernels().set_norm_fwd_blocks(128 if on else 0)),
-               "normgrid256": lambda on: (torch.cuda.synchronize(), kernels().set_norm_fwd_blocks(256 if on else 0)),
                "adamw_serial": lambda on: serial_adamw.__setitem__(0, bool(on)),
                "raster": lambda on: (torch.cuda.synchronize(), kernels().gemm_w4_set_group(-1 if on else 0))}
     configs = list(itertools.product([False, True], repeat=len(knobs)))

@@ -20,27 +20,6 @@ def rel(a, b):
     return ((a - b).norm() / (b.norm() + 1e-12)).item()
 
 
-@pytest.mark.parametrize("blocks", [1, 7, 128])
-def test_norm_fwd_grid_cap_bitwise(K, blocks):
-    """set_norm_fwd_blocks: rows in a grid stride over a capped grid give the default kernel's
-    output bitwise (add + norm, RMSNorm and LayerNorm, a row count not a multiple of the grid)."""
-    torch.manual_seed(3)
-    M, N = 1003, 4096
-    x = torch.randn(M, N, device="cuda").bfloat16()
-    d = torch.randn(M, N, device="cuda").bfloat16()
-    w = (1 + 0.1 * torch.randn(N, device="cuda")).bfloat16()
-    for ln in (False, True):
-        ref = K.add_norm_fwd(x, d, w, 1e-5, ln)
-        try:
-            K.set_norm_fwd_blocks(blocks)
-            got = K.add_norm_fwd(x, d, w, 1e-5, ln)
-        finally:
-            K.set_norm_fwd_blocks(0)
-        for a, b in zip(ref, got):
-            if a is not None and a.numel():
-                assert torch.equal(a, b)
-
-
 @pytest.mark.parametrize("M,N", [(1, 128), (7, 768), (2048, 4096), (33, 1024), (5, 8192), (300, 2560), (4099, 2048)])
 @pytest.mark.parametrize("ln", [False, True])
 def test_norm(K, M, N, ln):
