@@ -1643,6 +1643,7 @@ int g_fwd_pipe = 1;
 // hand-off (epilogue 2.0 -> 6.3 us) cost more than the balance gained; at S = 8192 it balanced
 // the CUs but the span stayed 746 us. profiles/r5_flash_fwd_timeline_khalf.log.)
 long long* g_fwd_prof = nullptr;
+long g_fwd_prof_rows = 0;  // rows of the probe buffer (checked against the grid at launch)
 
 // dQ key split (see flash_bwd_dq_kernel): -1 default (on), 0 off, 1 on (flash_set_dq_split, for A/B).
 int g_dq_split = -1;
@@ -1740,6 +1741,8 @@ std::tuple<at::Tensor, at::Tensor> flash_fwd(const at::Tensor& qk, const at::Ten
                      cptr<bf16_t>(qkv), mptr<bf16_t>(out), mptr<float>(lse), B, (int)S, (int)Hq,   \
                      (int)Hkv, sl2, ldqk, g_fwd_prof)
   const bool pipe = !split && g_fwd_pipe >= 1;
+  TORCH_CHECK(g_fwd_prof == nullptr || !pipe || (long)grid.x <= g_fwd_prof_rows,
+              "flash_set_fwd_prof: the buffer needs ", grid.x, " rows of 8 int64");
   FT_DISPATCH_E16(qk.scalar_type(), {
     if (D == 128) {
       if (split) FT_FWD(128, 2); else if (pipe) FT_FWD_PIPE(128); else FT_FWD(128, 1);
@@ -1914,8 +1917,10 @@ void flash_set_fwd_prof(const std::optional<at::Tensor>& buf) {
   if (buf.has_value()) {
     TORCH_CHECK(buf->scalar_type() == at::kLong && buf->is_contiguous(), "flash_set_fwd_prof: int64 buffer");
     g_fwd_prof = reinterpret_cast<long long*>(buf->data_ptr<int64_t>());
+    g_fwd_prof_rows = buf->numel() / 8;
   } else {
     g_fwd_prof = nullptr;
+    g_fwd_prof_rows = 0;
   }
 }
 void flash_set_kv_split(int64_t v) { g_kv_split = (int)v; }

@@ -8,8 +8,13 @@ namespace {
 
 using namespace ftw4;
 
+long long* g_prof = nullptr;  // per-workgroup stamps (gemm_w4_set_prof): W4Args::prof of every launch
+long g_prof_rows = 0;         // rows of that buffer (checked against the grid at launch)
+
 void launch(at::ScalarType st_, int nj, const W4Args& p, int epi, hipStream_t st, bool at_ = false,
             bool bt = false) {
+  TORCH_CHECK(p.prof == nullptr || (long)p.tiles_m * p.tiles_n * (p.splits > 1 ? p.splits : 1) <= g_prof_rows,
+              "gemm_w4_set_prof: the buffer needs one row of 8 int64 per workgroup");
   // the step's layouts: forward (K-contiguous both), dX (k-major B), dW (k-major both)
   TORCH_CHECK(!at_ || bt, "gemm_w4: k-major A needs a k-major B (the dW layout)");
   if (at_)
@@ -122,7 +127,6 @@ int* splitk_ticks(const c10::Device& dev, hipStream_t st, long n) {
 // workspace alive until the launch is enqueued (the caching allocator orders its reuse on the
 // stream). Falls back to one workgroup per tile where the split cannot run.
 int g_dbg = 0;  // timing probes (gemm_w4_set_dbg): W4Args::dbg of every launch
-long long* g_prof = nullptr;  // per-workgroup stamps (gemm_w4_set_prof): W4Args::prof of every launch
 // Grouped tile raster (W4Args::group, tile_of): the XCD's 32 concurrent tiles as a G x 32/G block.
 // -1 (default): 8 for the dW layout (k-major A), 4 otherwise; >= 0 forces (0: the plain raster).
 // Measured per 8B product (scripts/w4_raster_bench.py, profiles/r5_w4_raster_sweep2.log): w13 dW
@@ -423,8 +427,10 @@ void gemm_w4_set_prof(const std::optional<at::Tensor>& buf) {
   if (buf.has_value()) {
     TORCH_CHECK(buf->scalar_type() == at::kLong && buf->is_contiguous(), "gemm_w4_set_prof: int64 buffer");
     g_prof = reinterpret_cast<long long*>(buf->data_ptr<int64_t>());
+    g_prof_rows = buf->numel() / 8;
   } else {
     g_prof = nullptr;
+    g_prof_rows = 0;
   }
 }
 

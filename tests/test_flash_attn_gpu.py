@@ -303,3 +303,12 @@ def test_flash_fwd_timing_probe():
     assert (p[:, 0] > 0).all()
     assert (p[:, 1] >= p[:, 0]).all() and (p[:, 2] >= p[:, 1]).all() and (p[:, 3] >= p[:, 2]).all()
     assert sorted(set((p[:, 6] // 4).tolist())) == list(range(S // 128))
+    small = torch.zeros(3, 8, dtype=torch.int64, device="cuda")  # fewer rows than blocks
+    try:
+        K.flash_set_fwd_split(0)
+        K.flash_set_fwd_prof(small)
+        with pytest.raises(RuntimeError, match="flash_set_fwd_prof"):
+            K.flash_fwd(qk, qkv, S, Hq, Hkv, D)
+    finally:
+        K.flash_set_fwd_prof(None)
+        K.flash_set_fwd_split(-1)

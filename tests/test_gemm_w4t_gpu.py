@@ -222,6 +222,13 @@ def test_w4_timing_probe():
     p = buf.cpu()
     assert (p[:, 3] > 0).all()
     assert sorted(p[:, 6].tolist()) == list(range(buf.shape[0]))
+    small = torch.zeros(3, 8, dtype=torch.int64, device="cuda")  # fewer rows than workgroups
+    try:
+        k.gemm_w4_set_prof(small)
+        with pytest.raises(RuntimeError, match="gemm_w4_set_prof"):
+            k.gemm_w4_ex(a, True, b, True, M, N, Kd, None, False, None, 8, 1)
+    finally:
+        k.gemm_w4_set_prof(None)
 
 
 @pytest.mark.parametrize("group", [2, 3, 4, 8])
