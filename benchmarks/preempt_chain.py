@@ -80,6 +80,11 @@ def main():
                     help="delete a job's checkpoint once the next job has resumed from it AND written a "
                          "durable checkpoint of its own (an 8B chain holds at most two 48 GB checkpoints "
                          "on disk instead of one per job, and always one it can resume from)")
+    ap.add_argument("--prune-on-resume", action="store_true",
+                    help="delete a job's checkpoint as soon as the next job has resumed from it (a disk "
+                         "that holds ONE checkpoint, e.g. 79 GB for the 48 GB 8B file: the next save "
+                         "needs the space; a job that dies before its own save then has nothing to "
+                         "resume from -- the trade --prune-consumed avoids where two fit)")
     ap.add_argument("train_args", nargs=argparse.REMAINDER)
     a = ap.parse_args()
     extra = [x for x in a.train_args if x != "--"]
@@ -109,13 +114,13 @@ def main():
             return
         resumed = "Resuming training from training_step" in text
         own = "Checkpoint written:" in text or "[EXIT HANDLER] Checkpoint saved at step" in text
-        if resumed and own:
+        if resumed and (own or a.prune_on_resume):
             path = checkpoint_file(ck, prev)
             if os.path.exists(path):
                 os.remove(path)
             pruned.append(prev)
 
-    jobs = sim.run(a.jobs, prune if a.prune_consumed else None)
+    jobs = sim.run(a.jobs, prune if (a.prune_consumed or a.prune_on_resume) else None)
     rows, lost = [], 0
     prev = None
     for j in jobs:

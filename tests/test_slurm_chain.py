@@ -44,8 +44,10 @@ def test_usr1_resubmit_chain_x3(tmp_path):
         prev_saved = saved
 
 
-def test_preempt_chain_prunes_consumed_checkpoints(tmp_path):
-    """benchmarks/preempt_chain.py --prune-consumed (the 8B chain on a 79 GB disk): each job's
+@pytest.mark.parametrize("mode", ["--prune-consumed", "--prune-on-resume"])
+def test_preempt_chain_prunes_consumed_checkpoints(tmp_path, mode):
+    """benchmarks/preempt_chain.py --prune-consumed (after the next job's own durable save) and
+    --prune-on-resume (as soon as it resumed: a disk that holds one 8B checkpoint): each job's
     checkpoint is deleted once the next job has resumed from it; zero steps lost still holds."""
     import json
     import subprocess
@@ -54,7 +56,7 @@ def test_preempt_chain_prunes_consumed_checkpoints(tmp_path):
     ck = tmp_path / "ck"
     env = dict(os.environ, OMP_NUM_THREADS="2", PYTHONUNBUFFERED="1")
     r = subprocess.run([sys.executable, os.path.join(ROOT, "benchmarks", "preempt_chain.py"), "--jobs", "3",
-                        "--time", "14", "--signal-lead", "7", "--checkpoint-path", str(ck), "--prune-consumed", "--",
+                        "--time", "14", "--signal-lead", "7", "--checkpoint-path", str(ck), mode, "--",
                         "--device", "cpu", "--model", "tiny", "--synthetic-data", "--vocab-size", "256",
                         "--sequence-length", "32", "--logging-frequency", "50"],
                        env=env, capture_output=True, text=True, timeout=240)
