@@ -8,6 +8,3 @@ timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun
 tail -1 gpurun_out/r5u_smoke.log
 timeout -k 10 400 python -u bench.py --steps 20 --warmup 5 > gpurun_out/r5u_bench.log 2>&1 || exit 1
 tail -1 gpurun_out/r5u_bench.log | cut -c1-300
-timeout -k 10 120 python -u -m pytest tests/test_kernels_gpu.py -q -x -k "norm" --timeout 60 --timeout-method thread -p no:cacheprovider > gpurun_out/r5u_norm_tests.log 2>&1 && timeout -k 10 600 python -u scripts/ab_step.py --knobs normgrid --rounds 3 > gpurun_out/r5u_ab_normgrid.log 2>&1 || exit 1
-timeout -k 10 600 python -u scripts/ab_step.py --knobs normgrid256 --rounds 3 > gpurun_out/r5u_ab_normgrid256.log 2>&1 || exit 1
-grep best gpurun_out/r5u_ab_normgrid*.log
