@@ -128,12 +128,15 @@ int* splitk_ticks(const c10::Device& dev, hipStream_t st, long n) {
 // stream). Falls back to one workgroup per tile where the split cannot run.
 int g_dbg = 0;  // timing probes (gemm_w4_set_dbg): W4Args::dbg of every launch
 // Grouped tile raster (W4Args::group, tile_of): the XCD's 32 concurrent tiles as a G x 32/G block.
-// -1 (default): 8 for the dW layout (k-major A), 4 otherwise; >= 0 forces (0: the plain raster).
+// -1 (default): 8 for the dW layout (k-major A), 4 or 8 per entry otherwise; >= 0 forces (0: plain).
 // Measured per 8B product (scripts/w4_raster_bench.py, profiles/r5_w4_raster_sweep2.log): w13 dW
 // 392 -> 348 us, head dW 1823 -> 1682, head dX 1498 -> 1442, w2 / w13 forward 1.02x; the small
 // one-round products unchanged.
 int g_group = -1;
-int raster_group(bool a_t) { return g_group >= 0 ? g_group : (a_t ? 8 : 4); }
+// The forward NT entry (w2 / LM-head forward) and the SwiGLU-backward dX take 8 too (head forward
+// 1565 -> 1533 us, SwiGLU backward 224 -> 219 us; the other products tie,
+// profiles/r5_w4_raster_sweep3.log); the plain dX and the fused QKV / SwiGLU forwards take 4.
+int raster_group(bool a_t, int dflt = 4) { return g_group >= 0 ? g_group : (a_t ? 8 : dflt); }
 
 void setup_split(W4Args& p, int splits, int nj, const at::Tensor& like, at::Tensor& ws_hold) {
   p.dbg = g_dbg;
@@ -183,7 +186,7 @@ at::Tensor gemm_nt_w4(const at::Tensor& a, const at::Tensor& b, const std::optio
   }
   W4Args p{};
   p.prof = g_prof;
-  p.group = raster_group(false);
+  p.group = raster_group(false, 8);
   p.a = cptr<bf16_t>(a);
   p.b = cptr<bf16_t>(b);
   p.c = mptr<bf16_t>(c);
@@ -391,7 +394,7 @@ at::Tensor gemm_swiglu_bwd_w4(const at::Tensor& dy, const at::Tensor& w2, const 
   auto dgu = at::empty({M, 2 * F}, dy.options());
   W4Args p{};
   p.prof = g_prof;
-  p.group = raster_group(false);
+  p.group = raster_group(false, 8);
   p.a = cptr<bf16_t>(dy);
   p.b = cptr<bf16_t>(w2);
   p.c = mptr<bf16_t>(dgu);
