@@ -54,7 +54,8 @@ def parse():
     ap.add_argument("--seq-len", type=int, default=2048)
     ap.add_argument("--batch-size", type=int, default=1)
     ap.add_argument("--vocab-size", type=int, default=131072)
-    ap.add_argument("--bucket-mb", type=float, default=256.0)
+    ap.add_argument("--bucket-mb", type=float, default=None,
+                    help="gradient / optimizer bucket MiB (default: 64 on one GPU, 256 under DP)")
     ap.add_argument("--ckpt-dir", default="", help="directory for the checkpoint-save measurement "
                     "(default: $FT_BENCH_CKPT_DIR or <tmpdir>/ft_bench_ckpt)")
     ap.add_argument("--no-ckpt", action="store_true", help="skip the checkpoint-save measurement")

@@ -62,6 +62,8 @@ from ..models.flat import FlatParamSpace
 from ..ops.grad_sink import GradSink
 
 MODES = ("local", "allreduce", "zero1")
+LOCAL_BUCKET_MB = 64.0
+DP_BUCKET_MB = 256.0
 PARTIALS_PER_BUCKET = 512
 # A/B switch (scripts/ab_step.py): take every bucket's sum of squares in one pass after
 # backward instead of as each bucket completes (the default overlaps them with backward)
@@ -159,7 +161,7 @@ def make_buckets(flat: FlatParamSpace, bucket_mb: float, solo=()) -> List[Bucket
 
 
 class GradReducer:
-    def __init__(self, flat: FlatParamSpace, extra_sinks: List[GradSink], bucket_mb: float = 256.0,
+    def __init__(self, flat: FlatParamSpace, extra_sinks: List[GradSink], bucket_mb: Optional[float] = None,
                  mode: Optional[str] = None, group=None, overlap: Optional[bool] = None,
                  sparse_embedding: bool = True, reduce_dtype: str = "native"):
         """``reduce_dtype``: "native" (or "bf16") reduces the gradient buckets in their own
@@ -197,6 +199,12 @@ class GradReducer:
         # with it: GPT-2-medium 15.07 -> 14.97 ms/step, GPT-2-small and 8B unchanged
         # (profiles/r2_emb_solo_bucket_ab.log; FT_EMB_SOLO_BUCKET=0 restores the plain cut)
         solo_emb = self.sparse_embedding or (os.environ.get("FT_EMB_SOLO_BUCKET", "1") == "1" and emb in flat.slots)
+        if bucket_mb is None:
+            # one GPU: buckets are only the optimizer's launch / gating unit -- finer gating lets the
+            # next forward start each layer sooner (8B step 98.4 -> 97.0-97.2 ms from 256 to 16-64 MiB,
+            # profiles/r5_bucket_size.log); under DP they are the collectives' size (256 MiB: the
+            # xGMI chunk arithmetic in docs/PERFORMANCE.md)
+            bucket_mb = LOCAL_BUCKET_MB if mode == "local" else DP_BUCKET_MB
         self.buckets = make_buckets(flat, bucket_mb, solo=(emb,) if solo_emb else ())
         if self.sparse_embedding:
             es = flat.slots[emb]

@@ -164,8 +164,9 @@ def build_parser() -> argparse.ArgumentParser:
     parser.add_argument(
         "--dp-bucket-mb",
         type=float,
-        default=256.0,
-        help="Gradient all-reduce bucket size in MiB (data parallel)",
+        default=None,
+        help="Gradient bucket size in MiB: the all-reduce / reduce-scatter unit under data parallelism "
+             "(default 256) and the optimizer's launch / gating unit on one GPU (default 64)",
     )
     parser.add_argument(
         "--dp-mode",

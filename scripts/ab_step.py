@@ -64,7 +64,7 @@ def main():
     torch.cuda.set_device(dev)
     margs = model_args_for(a.model, vocab_size=a.vocab_size, seq_len=a.seq_len)
     model = build_model(margs, dev, torch.bfloat16, seed=1234)
-    red = GradReducer(model.flat, model.sinks_in_backward_order(), bucket_mb=256.0)
+    red = GradReducer(model.flat, model.sinks_in_backward_order())  # bench.py's default buckets
     opt = FlatAdamW(model.parameters(), model.flat, lr=5e-5, max_grad_norm=1.0, reducer=red)
     model.gate = opt.gate
     sched = build_lr_scheduler(opt, 100)
