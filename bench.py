@@ -196,10 +196,6 @@ def main():
     if a.graph:
         if K > 1 or dev.type != "cuda":
             raise SystemExit("--graph: GPU ranks, no gradient accumulation")
-        if red.mode == "zero1":
-            # ZeRO-1's gated parameter all-gathers crashed under capture (1-rank RCCL, round 5):
-            # the captured DP step is the all-reduce mode's
-            raise SystemExit("--graph under data parallelism: --dp-mode allreduce")
         from fault_tolerant_llm_training_amd.graphs import GraphedStep
 
         def fwd_bwd(tok, lab):

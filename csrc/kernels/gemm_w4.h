@@ -203,10 +203,16 @@ struct W4Args {
   // wave store) and raise flag tick[8 tile + slice]; the last slice adds them in slice order to
   // its own in the epilogue (fixed order: deterministic) and re-arms the flags for the next launch.
   int splits;
-  int dbg;               // timing probes only (gemm_w4_set_dbg): bit 0 = skip the epilogue's global stores
+  int dbg;               // timing probes only (gemm_w4_set_dbg): bit 0 = skip the epilogue's global stores;
+                         // bit 1 (tests): split-K producers never raise their flags (the timeout path)
   long long* prof;       // timing probe (gemm_w4_set_prof; scripts/w4_timeline.py): [grid][8] int64
   int* tick;             // [8 * tiles] int32, zero between launches (per device and stream)
   float* ws;             // [tiles * (S - 1) * 256 * BN] fp32
+  // split-K hand-off that never completed (a producer lost, > spin polls): the consumer adds 1 to
+  // *err (read by gemm_w4_splitk_errors), writes NaN for the whole tile (so the step's non-finite
+  // guard skips the update and the trainer stops on it) and re-arms only the flags it saw raised
+  int* err;
+  int spin;              // consumer poll bound (2^22 ~ seconds; tests lower it)
 };
 
 // (tm, tn) of workgroup bid (returned by value: through references the pair went to scratch)
@@ -446,6 +452,10 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(W4Args p) {
 
   // LDS-DMA sources. Instruction q of wave w fills image piece P = q * 4 + w (bytes [P KiB, +1 KiB)),
   // lane L its 16 B at P KiB + 16 L; the lane's source is the element that image slot holds.
+  // A tail tile (M % 256: the GPT-2 LM-head dW, M = V = 50304) clamps the sources of its rows past M
+  // onto row M - 1 (K-contiguous A) / the last 8-row chunk (k-major A, M % 8): every load stays
+  // inside A, and those rows' results are never stored.
+  const int mlast = min(BM, p.M - m0) - 1;  // last valid tile row
   Ctx c;
   c.wid = wid;
   c.lds0 = __builtin_amdgcn_readfirstlane(lds_u32(smem));
@@ -459,14 +469,14 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(W4Args p) {
       const int off = (q * 4 + wid) * PIECE + lane * 16;
       const int k = off / RBA, cp = (off % RBA) >> 4;
       const int gc = cp ^ (2 * tsw<RBA>(k));
-      c.voA[q] = (unsigned)(((long)k * p.lda + gc * 8) * 2);
+      c.voA[q] = (unsigned)(((long)k * p.lda + min(gc * 8, mlast - 7)) * 2);
     }
   } else {
     // [256 rows][64 k], 128-B rows: lane's 16-B chunk (lane & 7) holds global chunk (lane & 7) ^ (row & 7)
     c.srdA = make_srd(p.a + (long)m0 * p.lda + k0);
     c.stepA = (unsigned)(BK * 2);
 #pragma unroll
-    for (int q = 0; q < 8; ++q) c.voA[q] = (unsigned)(((q * 32 + lrow) * p.lda + lch * 8) * 2);
+    for (int q = 0; q < 8; ++q) c.voA[q] = (unsigned)((min(q * 32 + lrow, mlast) * p.lda + lch * 8) * 2);
   }
   if constexpr (BT) {
     c.srdB = make_srd(p.b + n0 + k0 * p.ldb);
@@ -594,10 +604,11 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(W4Args p) {
     }
   };
 
-  // (the dW layout, k-major A, has no split-K: its tile grids fill the chip, and the extra live
-  // registers of the hand-off pushed its widest tile into scratch)
+  // (the dW layout, k-major A, splits only its narrow tile: the GPT-2-sized weight gradients, whose
+  // 18-96-tile grids cannot fill 256 CUs; the 8B grids fill the chip unsplit)
   const float4* split_slot = nullptr;  // split-K consumer: slice 0's partial (uniform)
-  if constexpr ((EPI == W4_STORE || EPI == W4_RES) && !AT) {
+  int split_lost = 0;                  // ... and its hand-off timed out: the tile is written as NaN
+  if constexpr ((EPI == W4_STORE || EPI == W4_RES) && (!AT || NJ <= 4)) {
     if (nsplit > 1) {  // uniform (2 .. 8: host-checked)
       // Static roles, wave-uniform control flow (no single-lane branches near the 256 live
       // accumulators: those made the compiler copy them to VGPRs and spill): slices 0 .. S-2 (the
@@ -622,7 +633,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(W4Args p) {
                          : "memory");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        if (wid == 0) {  // the whole wave (one address, one value)
+        if (wid == 0 && !(p.dbg & 2)) {  // the whole wave (one address, one value)
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           __hip_atomic_store(flags + ks, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -630,22 +641,33 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(W4Args p) {
         probe_end();
         return;
       }
+      __shared__ int lost;  // a producer's flag never came
       if (wid == 0) {
-        // lane l watches slice (l & 7)'s flag; bounded (2^22 polls, a few seconds) so a broken
-        // hand-off cannot hang the GPU
+        // lane l watches slice (l & 7)'s flag; bounded (p.spin polls, a few seconds by default) so
+        // a broken hand-off cannot hang the GPU
         int* fl = flags + (lane & 7);
         const bool watch = (lane & 7) < nsplit - 1;
-        for (int n = 0; n < (1 << 22); ++n) {
-          const int v = __hip_atomic_load(fl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        int v = 0;
+        for (int n = 0; n < p.spin; ++n) {
+          v = __hip_atomic_load(fl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           if (__all(!watch || v != 0)) break;
           __builtin_amdgcn_s_sleep(4);
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        __hip_atomic_store(fl, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-armed (all 8)
+        // re-arm only the flags seen raised: one never seen may still be raised by a late producer,
+        // and the error word makes that launch (and the buffer) visibly bad instead of silently
+        const bool miss = watch && v == 0;
+        if (!miss) __hip_atomic_store(fl, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const bool any = __any(miss);
+        if (lane == 0) {
+          lost = any ? 1 : 0;
+          if (any) __hip_atomic_fetch_add(p.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       split_slot = slot - (long)ks * SLOT;  // slice 0's partial; the epilogue adds them as it converts
+      split_lost = __builtin_amdgcn_readfirstlane(lost);
     }
   }
 
@@ -685,6 +707,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(W4Args p) {
           v[1] = ps[j].y + v[1];
           v[2] = ps[j].z + v[2];
           v[3] = ps[j].w + v[3];
+          if (split_lost) v = f32x4_t{__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""), __builtin_nanf("")};
         }
         uint2 pk;
         pk.x = pk2<E>(v[0], v[1]);
@@ -737,8 +760,9 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(W4Args p) {
 #pragma unroll 4
     for (int rr = 0; rr < 32; ++rr) {
       const int row = rr * 4 + (lane >> 4);
-      uint4 v = *reinterpret_cast<const uint4*>(wl + row * 256 + ((cc ^ (row & 15)) << 4));
       const long gm = m0 + wm * 128 + row;
+      if (gm >= p.M) continue;  // tail tile: rows past M are not stored (nor summed)
+      uint4 v = *reinterpret_cast<const uint4*>(wl + row * 256 + ((cc ^ (row & 15)) << 4));
       // W4_SWIGLU: wave column half 0 holds g (gu columns [0, F)), half 1 holds u ([F, 2F))
       const int gn = EPI == W4_SWIGLU ? (wn ? p.ffn : 0) + f0 + cc * 8 : n0 + wn * NW + cc * 8;
       if constexpr (EPI == W4_RES) {

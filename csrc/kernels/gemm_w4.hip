@@ -31,7 +31,7 @@ void launch(at::ScalarType st_, int nj, const W4Args& p, int epi, hipStream_t st
 // unit of work (8B qkv dW 6144 x 4096 x 2048: 116.4 us at 128 columns in 3 rounds vs 99.9 us at
 // 256 in 2, profiles/r4_w4_dw_nj_probe.log).
 int pick_nj(long M, long N, bool kmajor_a = false) {
-  const long tm = M / BM;
+  const long tm = (M + BM - 1) / BM;
   int best = 0;
   double best_cost = 1e30;
   for (int nj : {8, 7, 6, 4}) {
@@ -66,10 +66,12 @@ struct Plan {
 // Per-shape tile width and split: minimise rounds of 256 workgroups x per-workgroup work, with the
 // tile widths' relative main-loop rates (eff) and a fixed epilogue / split hand-off cost per tile in
 // K-tile units (the split's first half writes 4 B per output element, the second reads them).
+// The dW layout (k-major A) splits only its 128-wide tile (gemm_w4.h: the wider k-major tiles keep
+// no registers for the hand-off): the GPT-2-sized weight gradients, 18-96 tiles at 2048 tokens.
 Plan pick_plan(long M, long N, long K, bool kmajor_a, bool kmajor_b) {
-  const long tm = M / BM, nkt = K / BK;
+  const long tm = (M + BM - 1) / BM, nkt = K / BK;
   Plan best{pick_nj(M, N, kmajor_a), 1};
-  if (g_splitk_mode == 0 || best.nj == 0 || kmajor_a) return best;
+  if (g_splitk_mode == 0 || best.nj == 0) return best;
   // per slice: its K-tiles, the epilogue (~3 K-tiles), the partial's store (~3) and, for the last
   // slice, reading the S - 1 partials (~3 each)
   auto cost = [&](int nj, int sp) {
@@ -80,10 +82,14 @@ Plan pick_plan(long M, long N, long K, bool kmajor_a, bool kmajor_b) {
   };
   double bc = cost(best.nj, 1);
   for (int nj : {8, 7, 6, 4}) {
-    if (N % (32L * nj)) continue;
+    if (N % (32L * nj) || (kmajor_a && nj != 4)) continue;
     const long tiles = tm * (N / (32L * nj));
-    for (int sp : {2, 4, 8}) {
-      if (nkt / sp < 16 || (K / (2 * BK)) < sp) continue;
+    // slices of >= 16 K-tiles; >= 8 for grids under half the chip with K >= 2048 (GPT-2 sizes:
+    // there the split's hand-off is cheaper than idle CUs, profiles/r5_gpt2_gemm_probe2.log; the
+    // 1024-deep ones gain nothing from a split)
+    const long min_kt = (tiles < 128 && nkt >= 32) ? 8 : 16;
+    for (int sp : {2, 3, 4, 8}) {
+      if (nkt / sp < min_kt || (K / (2 * BK)) < sp) continue;
       if (tiles * sp > 256) continue;  // one round: every slice co-resident with its tile's others
       if (g_splitk_mode == 2 && sp != 2) continue;
       const double c = cost(nj, sp);
@@ -98,35 +104,44 @@ Plan pick_plan(long M, long N, long K, bool kmajor_a, bool kmajor_b) {
 
 // Split-K hand-off flags: one zeroed int32 buffer per (device, stream), grown on demand and kept
 // (each tile's last slice re-arms its flags, so the buffer is zero between launches; launches on
-// one stream are ordered, two streams never share flags). Under stream capture nothing is
-// allocated: the capture stream borrows the device's first buffer (a captured graph replays on
-// the stream that ran the eager steps before it, so the two never run at once), else the caller
-// runs without split (nullptr) -- and a graph then sums in another order than the eager step.
+// one stream are ordered, two streams never share flags). The buffer's last word counts hand-offs
+// that timed out (W4Args::err, gemm_w4_splitk_errors). Nothing can be allocated under stream
+// capture: a graph's capture stream gets its own buffer beforehand (gemm_w4_prepare_capture, from
+// GraphedStep.prime), so its replays never share flags with eager launches on any stream. Without
+// one the product runs unsplit (and says so once): a graph would then sum in another order than
+// the eager step.
+std::mutex g_tick_mu;
+std::map<std::pair<int, hipStream_t>, at::Tensor> g_tick_bufs;
+constexpr long TICKS = 65536;  // >= 8 x the tiles of any split plan (<= 256 workgroups) + the error word
+
+at::Tensor& tick_buffer_locked(const c10::Device& dev, hipStream_t st) {
+  auto it = g_tick_bufs.find({dev.index(), st});
+  if (it != g_tick_bufs.end()) return it->second;
+  static std::vector<at::Tensor> keep;  // never freed: a captured graph holds its pointer
+  at::Tensor b = at::zeros({TICKS}, at::TensorOptions().device(dev).dtype(at::kInt));
+  keep.push_back(b);
+  return g_tick_bufs[{dev.index(), st}] = b;
+}
+
 int* splitk_ticks(const c10::Device& dev, hipStream_t st, long n) {
-  static std::mutex mu;
-  static std::map<std::pair<int, hipStream_t>, at::Tensor> bufs;
-  static std::map<int, at::Tensor> first;
-  std::lock_guard<std::mutex> lock(mu);
-  auto it = bufs.find({dev.index(), st});
-  if (it != bufs.end() && it->second.numel() >= n) return it->second.data_ptr<int>();
+  std::lock_guard<std::mutex> lock(g_tick_mu);
+  TORCH_CHECK(n < TICKS, "gemm_w4: split-K flag buffer too small for ", n, " flags");
+  auto it = g_tick_bufs.find({dev.index(), st});
+  if (it != g_tick_bufs.end()) return it->second.data_ptr<int>();
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) {
-    auto f = first.find(dev.index());
-    return (f != first.end() && f->second.numel() >= n) ? f->second.data_ptr<int>() : nullptr;
+    TORCH_WARN_ONCE("gemm_w4: split-K product captured on a stream without a prepared flag buffer "
+                    "(gemm_w4_prepare_capture): it runs unsplit inside the graph");
+    return nullptr;
   }
-  static std::vector<at::Tensor> keep;  // never freed: a captured graph may hold a replaced one
-  at::Tensor b = at::zeros({std::max(n, 65536L)}, at::TensorOptions().device(dev).dtype(at::kInt));
-  keep.push_back(b);
-  bufs[{dev.index(), st}] = b;
-  auto f = first.find(dev.index());
-  if (f == first.end() || f->second.numel() < b.numel()) first[dev.index()] = b;
-  return b.data_ptr<int>();
+  return tick_buffer_locked(dev, st).data_ptr<int>();
 }
 
 // Sets p.splits (1 or 2) and the split's hand-off words / fp32 workspace; `ws_hold` keeps the
 // workspace alive until the launch is enqueued (the caching allocator orders its reuse on the
 // stream). Falls back to one workgroup per tile where the split cannot run.
 int g_dbg = 0;  // timing probes (gemm_w4_set_dbg): W4Args::dbg of every launch
+int g_spin = 1 << 22;  // split-K consumer poll bound (gemm_w4_set_spin: tests of the timeout path)
 // Grouped tile raster (W4Args::group, tile_of): the XCD's 32 concurrent tiles as a G x 32/G block.
 // -1 (default): 8 for the dW layout (k-major A), 4 or 8 per entry otherwise; >= 0 forces (0: plain).
 // Measured per 8B product (scripts/w4_raster_bench.py, profiles/r5_w4_raster_sweep2.log): w13 dW
@@ -138,20 +153,22 @@ int g_group = -1;
 // profiles/r5_w4_raster_sweep3.log); the plain dX and the fused QKV / SwiGLU forwards take 4.
 int raster_group(bool a_t, int dflt = 4) { return g_group >= 0 ? g_group : (a_t ? 8 : dflt); }
 
-void setup_split(W4Args& p, int splits, int nj, const at::Tensor& like, at::Tensor& ws_hold) {
+void setup_split(W4Args& p, int splits, int nj, const at::Tensor& like, at::Tensor& ws_hold, bool a_t = false) {
   p.dbg = g_dbg;
   p.prof = g_prof;
   p.splits = 1;
   if (splits < 2) return;
   TORCH_CHECK(splits <= 8, "gemm_w4: split-K of 2 .. 8");
   TORCH_CHECK(p.K / (2 * BK) >= splits, "gemm_w4: split-K needs K / 128 >= splits");
-  TORCH_CHECK(p.lda == p.K, "gemm_w4: split-K is built for K-contiguous A (forward / dX)");
+  TORCH_CHECK(!a_t || nj == 4, "gemm_w4: split-K of the dW layout (k-major A) is built for the 128-wide tile");
   const long tiles = (long)p.tiles_m * p.tiles_n;
   int* t = splitk_ticks(like.device(), ft_stream(), 8 * tiles);
   if (t == nullptr) return;
   ws_hold = at::empty({tiles * (splits - 1) * BM * 32L * nj}, like.options().dtype(at::kFloat));
   p.splits = splits;
   p.tick = t;
+  p.err = t + (TICKS - 1);
+  p.spin = g_spin;
   p.ws = ws_hold.data_ptr<float>();
 }
 
@@ -233,7 +250,9 @@ at::Tensor gemm_w4_ex(const at::Tensor& a, bool a_t, const at::Tensor& b, bool b
   const Plan pl = nj > 0 ? Plan{(int)nj, (int)std::max<int64_t>(splits, 1)} : pick_plan(M, N, K, a_t, b_t);
   const int NJ = pl.nj;
   TORCH_CHECK(NJ == 8 || NJ == 7 || NJ == 6 || NJ == 4, "gemm_w4_ex: no tile width fits N = ", N);
-  TORCH_CHECK(M % BM == 0 && N % (32 * NJ) == 0 && K % (2 * BK) == 0 && K > 0, "gemm_w4_ex: M % 256, N % ",
+  // M % 256 != 0 runs a tail tile (its rows past M clamped on load, not stored): the GPT-2 LM-head
+  // dW at V = 50304 (k-major A reads 8-row chunks: M % 8)
+  TORCH_CHECK(M % 8 == 0 && M > 0 && N % (32 * NJ) == 0 && K % (2 * BK) == 0 && K > 0, "gemm_w4_ex: M % 8, N % ",
               32 * NJ, ", K % 128 (got ", M, " ", N, " ", K, ")");
   // 32-bit buffer offsets: the whole operand (a K-tile advance is a scalar offset) under 4 GiB
   TORCH_CHECK(M * K * 2 < (1L << 32) && N * K * 2 < (1L << 32), "gemm_w4_ex: operand over 4 GiB");
@@ -262,7 +281,7 @@ at::Tensor gemm_w4_ex(const at::Tensor& a, bool a_t, const at::Tensor& b, bool b
   p.M = M;
   p.N = N;
   p.K = K;
-  p.tiles_m = M / BM;
+  p.tiles_m = (M + BM - 1) / BM;
   p.tiles_n = N / (32 * NJ);
   p.nfast = M > N;  // keep the larger operand's panels inside one XCD
   p.group = raster_group(a_t);
@@ -275,7 +294,7 @@ at::Tensor gemm_w4_ex(const at::Tensor& a, bool a_t, const at::Tensor& b, bool b
     p.part_n = (int)part->numel();
   }
   at::Tensor ws;
-  setup_split(p, pl.splits, NJ, a, ws);
+  setup_split(p, pl.splits, NJ, a, ws, a_t);
   launch(a.scalar_type(), NJ, p, accumulate ? W4_RES : W4_STORE, ft_stream(), a_t, b_t);
   FT_LAUNCH_CHECK();
   return c;
@@ -422,6 +441,31 @@ int64_t gemm_w4_pick(int64_t M, int64_t N) { return pick_nj(M, N); }
 // FT_W4_SPLITK at run time (A/B): 0 off, 1 automatic, 2 forced where it fits
 void gemm_w4_set_splitk(int64_t mode) { g_splitk_mode = (int)mode; }
 
+// Before a stream capture: the capture stream (current stream) gets its own split-K flag buffer,
+// so the graph's split products keep their split (same summation order as the eager step) and
+// never share flags with eager launches (graphs.GraphedStep.prime).
+void gemm_w4_prepare_capture() {
+  const auto cur = at::hip::getCurrentHIPStreamMasqueradingAsCUDA();
+  std::lock_guard<std::mutex> lock(g_tick_mu);
+  tick_buffer_locked(cur.device(), cur.stream());
+}
+
+// Split-K hand-offs that timed out since the last reset, summed over every flag buffer (a device
+// sync per buffer: diagnostics / tests, not the step).
+int64_t gemm_w4_splitk_errors(bool reset) {
+  std::lock_guard<std::mutex> lock(g_tick_mu);
+  int64_t n = 0;
+  for (auto& kv : g_tick_bufs) {
+    at::Tensor w = kv.second.narrow(0, TICKS - 1, 1);
+    n += w.item<int>();
+    if (reset) w.zero_();
+  }
+  return n;
+}
+
+// split-K consumer poll bound (tests of the timeout path; default 2^22)
+void gemm_w4_set_spin(int64_t n) { g_spin = (int)std::max<int64_t>(1, n); }
+
 // timing probes only (scripts/w4_overhead_probe.py): bit 0 skips the store / residual epilogues'
 // global stores (the output is left unwritten)
 void gemm_w4_set_dbg(int64_t v) { g_dbg = (int)v; }
@@ -452,6 +496,9 @@ TORCH_LIBRARY_FRAGMENT(ftamd, m) {
       &gemm_w4_ex);
   m.def("gemm_w4_plan(int M, int N, int K, bool a_t=False, bool b_t=False) -> int[]", &gemm_w4_plan);
   m.def("gemm_w4_set_splitk(int mode) -> ()", &gemm_w4_set_splitk);
+  m.def("gemm_w4_prepare_capture() -> ()", &gemm_w4_prepare_capture);
+  m.def("gemm_w4_splitk_errors(bool reset=False) -> int", &gemm_w4_splitk_errors);
+  m.def("gemm_w4_set_spin(int n) -> ()", &gemm_w4_set_spin);
   m.def("gemm_w4_set_dbg(int v) -> ()", &gemm_w4_set_dbg);
   m.def("gemm_w4_set_group(int v) -> ()", &gemm_w4_set_group);
   m.def("gemm_w4_set_prof(Tensor? buf) -> ()", &gemm_w4_set_prof);

@@ -24,6 +24,7 @@ from typing import Callable, Optional
 
 import torch
 
+from ._native import kernels
 from .ops.functional import join_dw_stream
 
 
@@ -37,12 +38,17 @@ class GraphedStep:
         self.lab: Optional[torch.Tensor] = None
         self.loss: Optional[torch.Tensor] = None
         self.pending = False  # a backward whose optimizer step has not run yet
+        self.cap_stream: Optional[torch.cuda.Stream] = None
+        # data parallel: every collective of the step on the reducer's side stream (the form RCCL
+        # collectives capture in: ddp.GradReducer.single_stream)
+        reducer.single_stream = bool(reducer.comm)
 
     def _join(self) -> None:
         cur = torch.cuda.current_stream()
         join_dw_stream()
         if self.red.side is not None:
             cur.wait_stream(self.red.side)
+
 
     def _opt_step(self) -> None:
         self.opt.clip_grad_norm_(self.opt.max_grad_norm)
@@ -68,7 +74,14 @@ class GraphedStep:
         self.opt.graph_mode = True
         g = torch.cuda.CUDAGraph()
         sc0 = self.opt.step_count
-        with torch.cuda.graph(g):
+        if self.cap_stream is None:
+            # one capture stream per GraphedStep, with its own split-K hand-off flags (allocated
+            # here: nothing can be allocated during capture), so the captured split products keep
+            # the eager step's summation order and never share flags with an eager launch
+            self.cap_stream = torch.cuda.Stream()
+            with torch.cuda.stream(self.cap_stream):
+                kernels().gemm_w4_prepare_capture()
+        with torch.cuda.graph(g, stream=self.cap_stream):
             self._opt_step()  # (its host-side step count is reset below; hyper is read on device)
             self.loss = self.fwd_bwd(self.tok, self.lab)
             self._join()

@@ -210,6 +210,13 @@ class FlatAdamW(torch.optim.Optimizer):
                              self.overlap_blocks if r.overlap else 0)
                 if self.zero1 and r.dry_comm:
                     pass
+                elif self.zero1 and r.single_stream and r.overlap:
+                    # whole-step graph: the all-gather blocking on this (side) stream, right behind
+                    # the bucket's update (ddp.GradReducer.single_stream); the next forward waits
+                    # for its event
+                    dist.all_gather_into_tensor(f.params[b.lo : b.hi], r.param_shard(b), group=r.group)
+                    b.agevent.record()
+                    self.gate.add(b.lo, b.hi, b.agevent)
                 elif self.zero1:
                     work = dist.all_gather_into_tensor(f.params[b.lo : b.hi], r.param_shard(b),
                                                        group=r.group, async_op=True)

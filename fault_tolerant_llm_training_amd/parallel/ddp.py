@@ -114,7 +114,7 @@ def _copy_back(dst: torch.Tensor, src: torch.Tensor, temps) -> None:
 
 class Bucket:
     __slots__ = ("idx", "lo", "hi", "needed", "filled", "launched", "work", "part_lo", "part_hi",
-                 "shard_lo", "shard_len", "event", "sparse", "post")
+                 "shard_lo", "shard_len", "event", "agevent", "sparse", "post")
 
     def __init__(self, idx, lo, hi, needed):
         self.idx, self.lo, self.hi, self.needed = idx, lo, hi, needed
@@ -124,7 +124,8 @@ class Bucket:
         self.part_lo = self.part_hi = 0
         self.shard_lo = 0     # offset of this bucket's shard in the rank-local shard buffers
         self.shard_len = 0    # elements per rank
-        self.event = None
+        self.event = None     # launching stream: the bucket's last gradient kernel is enqueued
+        self.agevent = None   # single-stream mode: after the bucket's parameter all-gather (ZeRO-1)
         self.sparse = False   # reduced by the sparse embedding exchange, not a bucket collective
         self.post = None      # fp32 reduce: copies the reduced fp32 result back (after work.wait())
 
@@ -257,16 +258,27 @@ class GradReducer:
                 b.shard_lo = self.shard_numel
                 self.shard_numel += b.shard_len
         self.side = torch.cuda.Stream(device=flat.device) if self.overlap else None
+        self.comm = self.world > 1 or mode != "local"
+        # Single-stream collectives (set by graphs.GraphedStep for the whole-step HIP graph): every
+        # data-plane collective is issued BLOCKING (async_op=False) on the side stream, so RCCL runs
+        # it on that stream, ordered by events. Captured RCCL collectives spread over more than one
+        # stream -- ProcessGroupNCCL's internal stream of the async form plus ours, or two of ours --
+        # crash hipStreamEndCapture (SIGSEGV, ROCm 7 / RCCL 2.26: the reduce-scatter in backward
+        # plus the parameter all-gather after AdamW, i.e. ZeRO-1), while any number of them on ONE
+        # stream, with compute-stream round trips between them, capture and replay correctly
+        # (scripts/capture_collectives_probe.py, profiles/r6/capture_collectives_probe.log). Eager
+        # steps keep the async form: the collectives overlap the side stream's AdamW launches.
+        self.single_stream = False
         if not self.fused_sumsq:  # sinks shared with an earlier reducer: no stale partials
             for sink in list(flat.sinks.values()) + list(extra_sinks):
                 sink.part, sink.sq_done = None, False
         if self.cuda:
             for b in self.buckets:
                 b.event = torch.cuda.Event()
+                b.agevent = torch.cuda.Event()
         self._extra_sinks = list(extra_sinks)
         for sink in list(flat.sinks.values()) + list(extra_sinks):
             sink.hook = self._on_ready
-        self.comm = self.world > 1 or mode != "local"
         self._pending_sumsq: List[Bucket] = []
         self._next = 0            # index of the next bucket to launch (in-order launch)
         self.fault_after_buckets = 0  # fault-injection hook: raise after this many launches
@@ -304,6 +316,16 @@ class GradReducer:
             return t, d
         t_all = torch.empty(self.world * t.numel(), dtype=t.dtype, device=t.device)
         d_all = torch.empty(self.world * d.shape[0], d.shape[1], dtype=d.dtype, device=d.device)
+        if self.single_stream and self.overlap:  # on the side stream with every other collective
+            cur = torch.cuda.current_stream()
+            self.side.wait_stream(cur)
+            with torch.cuda.stream(self.side):
+                dist.all_gather_into_tensor(t_all, t, group=self.group)
+                dist.all_gather_into_tensor(d_all, d, group=self.group)
+            cur.wait_stream(self.side)
+            for x in (t, d, t_all, d_all):
+                x.record_stream(self.side)
+            return t_all, d_all
         dist.all_gather_into_tensor(t_all, t, group=self.group)
         dist.all_gather_into_tensor(d_all, d, group=self.group)
         return t_all, d_all
@@ -411,9 +433,39 @@ class GradReducer:
                 return
         self._launch_now(b)
 
+    def _collective_blocking(self, b: Bucket, grads: torch.Tensor) -> None:
+        """Bucket b's reduction issued blocking on the current (comm) stream: RCCL runs it there."""
+        if self.reduce_fp32:
+            src = grads.float()
+            if self.mode == "allreduce":
+                dist.all_reduce(src, op=dist.ReduceOp.SUM, group=self.group)
+                grads.copy_(src)
+            else:
+                out = src.new_empty(b.shard_len)
+                dist.reduce_scatter_tensor(out, src, op=dist.ReduceOp.SUM, group=self.group)
+                self.grad_shard(b).copy_(out)
+        elif self.mode == "allreduce":
+            dist.all_reduce(grads, op=dist.ReduceOp.SUM, group=self.group)
+        elif self.mode == "zero1":
+            dist.reduce_scatter_tensor(self.grad_shard(b), grads, op=dist.ReduceOp.SUM, group=self.group)
+
     def _launch_now(self, b: Bucket) -> None:
         b.launched = True
         grads = self.flat.grads[b.lo : b.hi]
+        if self.single_stream and self.overlap:
+            # whole-step graph: the side stream waits for the bucket, reduces it (blocking: RCCL runs
+            # on the side stream) and takes its sum of squares; the host never waits
+            side = self.side
+            b.event.record()
+            side.wait_event(b.event)
+            with torch.cuda.stream(side):
+                if not (b.sparse or self.dry_comm):
+                    self._collective_blocking(b, grads)
+                if SUMSQ_AT_END:
+                    self._pending_sumsq.append(b)
+                else:
+                    self._sumsq(self.grad_for_update(b), b)
+            return
         if b.sparse or self.dry_comm:
             pass  # sparse: summed by the embedding exchange inside the embedding backward
         elif self.reduce_fp32:

@@ -156,8 +156,10 @@ class _RankFault:
 
     Phases: ``data`` (OSError while fetching the batch), ``forward``, ``backward`` (OSError
     raised inside backward after the first gradient bucket was launched), ``optimizer``
-    (before ``optimizer.step()``), ``post`` (after the step), ``kill`` (SIGKILL itself) and
-    ``hang`` (sleep forever) at the start of the step."""
+    (before ``optimizer.step()``), ``post`` (after the step), ``kill`` (SIGKILL itself),
+    ``hang`` (sleep forever) at the start of the step, and ``peerloss`` (the step's boundary vote
+    raises :class:`PeerFailure`, as when a peer died). Under the whole-step HIP graph the
+    forward / backward / optimizer faults fire before the replay, which then runs poisoned."""
 
     def __init__(self, spec: str, rank: int):
         self.step = self.phase = None
@@ -268,12 +270,11 @@ def train(args) -> int:
         # The reference compiles the model (train.py:61-63) to cut launch overhead and fuse ops.
         # Here the ops are already fused gfx950 kernels; what is left to "compile" is the launch
         # sequence, and the MI355X-native form of that is the whole-step HIP graph (--hip-graph):
-        # on GPU ranks without gradient accumulation --compile turns it on (under DP the bucket
-        # collectives are captured into the graph; the per-step vote stays on the host, between
-        # replays). Host-side accumulation or the fp64 path cannot be captured: there the flag
-        # is accepted and logged as not applied.
-        graphable = model_dtype in (torch.bfloat16, torch.float16, torch.float32) and not (
-            info.distributed and args.dp_mode != "allreduce")
+        # on GPU ranks without gradient accumulation --compile turns it on (under DP -- ZeRO-1 or
+        # all-reduce -- the bucket collectives and ZeRO-1's parameter all-gathers are captured into
+        # the graph; the per-step vote stays on the host, between replays). Host-side accumulation
+        # or the fp64 path cannot be captured: there the flag is accepted and logged as not applied.
+        graphable = model_dtype in (torch.bfloat16, torch.float16, torch.float32)
         if device.type == "cuda" and max(1, int(args.grad_accum)) == 1 and graphable:
             logger.info("Using `torch.compile`")
             logger.info("`torch.compile` -> whole-step HIP graph capture (--hip-graph): the step's "
@@ -283,8 +284,7 @@ def train(args) -> int:
             logger.info("Using `torch.compile` — accepted for CLI compatibility, not applied: the step "
                         "already runs fused gfx950 kernels and the whole-step HIP graph needs GPU ranks "
                         "without gradient accumulation, in a dtype the HIP kernels run (bf16/fp16/fp32: "
-                        "the fp64 composed path synchronises with the host inside the step), and under "
-                        "data parallelism --dp-mode allreduce")
+                        "the fp64 composed path synchronises with the host inside the step)")
     model.train()
 
     # AdamW moments default to the model dtype like the reference, except under fp16: the second
@@ -480,6 +480,8 @@ def train(args) -> int:
         nonlocal pending_err
         if save_due:
             complete_pending()  # graph mode: the snapshot needs the last step's optimizer update
+        if fault.at(training_step, "peerloss"):  # test hook: this boundary's vote fails
+            raise fdist.PeerFailure(f"injected peer loss at the boundary before step {training_step}")
         sig = monitor.pending()
         err = 1.0 if pending_err is not None else 0.0
         upto = optimizer.step_count if (final or save_due) else optimizer.step_count - 1
@@ -518,10 +520,6 @@ def train(args) -> int:
     if args.hip_graph:
         if K > 1 or device.type != "cuda" or model_dtype not in (torch.bfloat16, torch.float16, torch.float32):
             raise ValueError("--hip-graph: --grad-accum 1, --device cuda, --model-dtype bf16/fp16/fp32")
-        if reducer.mode == "zero1":
-            # ZeRO-1's gated parameter all-gathers crashed under stream capture (1-rank RCCL test,
-            # round 5): the captured DP step is the all-reduce mode's
-            raise ValueError("--hip-graph under data parallelism: --dp-mode allreduce")
         from .graphs import GraphedStep
 
         inv_dev = torch.empty(1, dtype=torch.float32, device=device)  # static input of the graph
@@ -590,13 +588,37 @@ def train(args) -> int:
             if graphed is not None:
                 inv_dev.copy_(inv, non_blocking=True)
                 lr_now = optimizer.param_groups[0]["lr"]
-                if graphed.ready:
-                    if ckpt["engine"] is not None:
-                        ckpt["engine"].fence()  # the replay's optimizer must follow a pending snapshot
-                    loss = graphed.step(batch.inputs, batch.labels)  # optimizer(k-1) + fwd/bwd(k)
-                else:
-                    loss = graphed.prime(batch.inputs, batch.labels)  # eager fwd/bwd(k), capture
-                loss = loss.detach().clone()
+                # A failure of this rank's share of the step before the replay: the replay still
+                # runs, poisoned (NaN loss scale -> NaN gradients in every captured collective), so
+                # the peers' replays complete, every rank's non-finite guard skips the update and
+                # the vote stops everyone on this step -- the eager path's poison_and_complete.
+                for ph in ("forward", "backward", "optimizer"):
+                    try:
+                        fault.fire(training_step, ph)
+                    except Exception as e:  # noqa: BLE001
+                        logger.error(f"Training error at step {training_step} ({ph}, graph mode): {e!r}")
+                        pending_err = e
+                        inv_dev.fill_(float("nan"))
+                        break
+                try:
+                    if graphed.ready:
+                        if ckpt["engine"] is not None:
+                            ckpt["engine"].fence()  # the replay's optimizer must follow a pending snapshot
+                        loss = graphed.step(batch.inputs, batch.labels)  # optimizer(k-1) + fwd/bwd(k)
+                    else:
+                        loss = graphed.prime(batch.inputs, batch.labels)  # eager fwd/bwd(k), capture
+                    loss = loss.detach().clone()
+                except Exception as e:  # noqa: BLE001
+                    # capture / replay itself failed: its collectives cannot be completed from here
+                    # (they live inside the graph), so this rank leaves like a lost peer
+                    raise _FatalStepError(f"HIP graph {'replay' if graphed.ready else 'capture'} failed at "
+                                          f"step {training_step}: {e!r}") from e
+                if pending_err is None:
+                    try:
+                        fault.fire(training_step, "post")
+                    except Exception as e:  # noqa: BLE001 - after a complete step: nothing to poison
+                        logger.error(f"Training error at step {training_step} (post, graph mode): {e!r}")
+                        pending_err = e
                 phase = "graph"
             tok_all = batch.inputs.to(device, non_blocking=True) if graphed is None else None
             lab_all = batch.labels.to(device, non_blocking=True) if graphed is None else None
@@ -721,6 +743,13 @@ def train(args) -> int:
             complete = False
         if complete and info.distributed:
             try:
+                # graph mode: the last replay's backward has no optimizer step yet (it runs in the
+                # next replay). Its gradients are complete (drained above) and the all-reduce mode's
+                # optimizer issues no collective, so run it here: the file then records
+                # training_step with every one of its updates, as at a clean boundary. (ZeRO-1's
+                # optimizer all-gathers would wait on the lost peer; save_solo refuses that mode.)
+                if not optimizer.zero1:
+                    complete_pending()
                 rollback_to_first_bad()
                 step_now = training_step
                 with monitor.blocked():

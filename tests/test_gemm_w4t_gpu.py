@@ -203,6 +203,86 @@ def test_split_k_8b_head_dx_vs_fp32():
     assert torch.equal(c, K().gemm_w4_ex(a, False, b, True, M, N, Kd, None, False, None, 8, 2))
 
 
+@pytest.mark.parametrize("M", [768, 1160, 50304])
+@pytest.mark.parametrize("splits", [1, 2, 3, 4])
+def test_dw_split_k_and_tail_tile(M, splits):
+    """The dW layout (k-major A and B) split over K (the GPT-2-sized weight gradients: 18-96 tiles of
+    256 x 128 at 2048 tokens) and with a tail tile (M % 256 != 0: the GPT-2 LM-head dW at V = 50304):
+    exact on integer operands for every split, the rows past M untouched, the sum-of-squares partials
+    of the stored values only, the accumulate epilogue, and fp32-close on random operands."""
+    k = K()
+    torch.manual_seed(M + splits)
+    N, T = 768, 2048
+    if M == 50304 and splits not in (1, 3):
+        pytest.skip("the 50304 tail at two splits is enough")
+    at = ints(T, M) + (torch.arange(M, device="cuda") % 3).bfloat16()  # dY [T, M] read k-major
+    b = ints(T, N)
+    ref = at.float().t() @ b.float()
+    tiles = ((M + 255) // 256) * (N // 128)
+    part = torch.full((tiles + 5,), 7.0, device="cuda")  # slots past the grid are zeroed
+    big = torch.full((M + 64, N), 3.0, dtype=torch.bfloat16, device="cuda")  # rows past M: canary
+    out = big[:M]
+    k.gemm_w4_ex(at, True, b, True, M, N, T, out, False, part, 4, splits)
+    assert torch.equal(out.float(), ref.bfloat16().float())
+    assert (big[M:] == 3.0).all()
+    assert part[tiles:].abs().sum().item() == 0
+    sq = (out.float() ** 2).sum().item()
+    assert abs(part.sum().item() - sq) <= 1e-5 * sq
+    k.gemm_w4_ex(at, True, b, True, M, N, T, out, True, None, 4, splits)  # accumulate
+    assert torch.equal(out.float(), (2 * ref).bfloat16().float())
+    # random operands: fp32-close, bitwise reproducible, and split == unsplit within rounding
+    at.copy_(rnd(T, M))
+    b.copy_(rnd(T, N))
+    ref = at.float().t() @ b.float()
+    o1 = k.gemm_w4_ex(at, True, b, True, M, N, T, None, False, None, 4, splits)
+    o2 = k.gemm_w4_ex(at, True, b, True, M, N, T, None, False, None, 4, splits)
+    assert rel(o1, ref) < 4e-3 and torch.equal(o1, o2)
+
+
+def test_gpt2_plans_split_the_small_dw_grids():
+    """The automatic plan splits the GPT-2-sized weight gradients (128-wide tiles, K = 2048 tokens)
+    and the tail-tile head dW at V = 50304 gets a plan at all."""
+    plan = lambda M, N, Kd, at=True, bt=True: list(K().gemm_w4_plan(M, N, Kd, at, bt))  # noqa: E731
+    for M, N in [(2304, 768), (768, 768), (4096, 768), (768, 2048), (3072, 1024), (1024, 1024)]:
+        nj, sp = plan(M, N, 2048)
+        assert nj == 4 and sp > 1, (M, N, nj, sp)
+    assert plan(50304, 768, 2048)[0] > 0
+    assert plan(131072, 4096, 2048) == [8, 1]  # the 8B head dW: a full grid, unsplit
+
+
+@pytest.mark.parametrize("layout", ["fwd", "dx"])
+def test_split_k_lost_handoff_is_loud(layout):
+    """A split-K hand-off that never completes (test mode: the producers never raise their flags,
+    the consumer's poll bound lowered) is counted in the error word and writes NaN for the whole
+    tile -- the step's non-finite guard then skips the update -- instead of a silently wrong sum;
+    the flags it never saw raised are not re-armed, and the next normal launch is exact again."""
+    k = K()
+    torch.manual_seed(5)
+    M, N, Kd = 512, 512, 1024
+    a = ints(M, Kd)
+    if layout == "fwd":
+        b = ints(N, Kd)
+        ref = (a.float() @ b.float().t()).bfloat16()
+        run = lambda: k.gemm_nt_w4(a, b, None, None, 8, 2)  # noqa: E731
+    else:
+        b = ints(Kd, N)
+        ref = (a.float() @ b.float()).bfloat16()
+        run = lambda: k.gemm_w4_ex(a, False, b, True, M, N, Kd, None, False, None, 8, 2)  # noqa: E731
+    k.gemm_w4_splitk_errors(True)
+    try:
+        k.gemm_w4_set_spin(64)
+        k.gemm_w4_set_dbg(2)
+        bad = run()
+        torch.cuda.synchronize()
+    finally:
+        k.gemm_w4_set_dbg(0)
+        k.gemm_w4_set_spin(1 << 22)
+    assert torch.isnan(bad.float()).all()
+    assert k.gemm_w4_splitk_errors(True) == (M // 256) * (N // 256)
+    assert torch.equal(run(), ref)
+    assert k.gemm_w4_splitk_errors(False) == 0
+
+
 def test_w4_timing_probe():
     """gemm_w4_set_prof (scripts/w4_timeline.py): one exit stamp per workgroup, output unchanged."""
     k = K()
