@@ -346,22 +346,43 @@ at::Tensor gemm_qkv_rope_w4(const at::Tensor& x, const at::Tensor& w, const at::
   return c;
 }
 
+// SwiGLU tile width: 32 NJ columns = 16 NJ features of w1 and the same of w3; whole rounds of 256
+// tiles at the fewest columns per CU (the 8B F = 14336: NJ 7, 4 x 256 tiles; GPT-2-small F = 2048:
+// NJ 4, one round of 256; GPT-2-medium F = 2816: NJ 8, 176 tiles). 0: F fits no width.
+int pick_swiglu_nj(long M, long F) {
+  int best = 0;
+  double best_cost = 1e30;
+  for (int nj : {7, 8, 6, 4}) {
+    if (F % (16L * nj)) continue;
+    const long tiles = (M / BM) * (F / (16L * nj));
+    const double eff = nj == 8 ? 1.0 : nj == 7 ? 0.99 : nj == 6 ? 0.98 : 0.92;
+    const double cost = (double)((tiles + 255) / 256) * nj / eff;
+    if (cost < best_cost - 1e-9) {
+      best_cost = cost;
+      best = nj;
+    }
+  }
+  return best;
+}
+
 // Fused w1|w3 projection + SwiGLU (reference model.py:254 silu(w1 x) * w3 x): x [M, K],
 // w13 = [w1; w3] [2F, K] -> (gu [M, 2F] = x w13^T for the backward, a = silu(g) u [M, F],
 // a^T [F, M] for a weight gradient on transposed operands, empty when with_t is false).
-// 224-column tiles: 112 features of w1 and the same 112 of w3; M % 256, F % 112, K % 64.
+// 32 NJ-column tiles: 16 NJ features of w1 and the same of w3 (nj = 0: pick_swiglu_nj);
+// M % 256, F % (16 NJ), K % 128.
 std::tuple<at::Tensor, at::Tensor, at::Tensor> gemm_swiglu_w4(const at::Tensor& x, const at::Tensor& w13,
-                                                              bool with_t) {
+                                                              bool with_t, int64_t nj) {
   FT_CHECK_CUDA(x);
   TORCH_CHECK(x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kHalf, "gemm_swiglu_w4: bf16 / fp16");
   TORCH_CHECK(w13.scalar_type() == x.scalar_type(), "gemm_swiglu_w4: x / w13 dtype mismatch");
   FT_CHECK_CONTIG(x);
   FT_CHECK_CONTIG(w13);
   const long M = x.size(0), K = x.size(1), F2 = w13.size(0), F = F2 / 2;
-  constexpr int NJ = 7, NWC = 16 * NJ;
+  const int NJ = nj > 0 ? (int)nj : pick_swiglu_nj(M, F), NWC = 16 * NJ;
+  TORCH_CHECK(NJ == 8 || NJ == 7 || NJ == 6 || NJ == 4, "gemm_swiglu_w4: no tile width fits F = ", F);
   TORCH_CHECK(w13.size(1) == K && F2 % 2 == 0, "gemm_swiglu_w4: shape mismatch");
-  TORCH_CHECK(M % BM == 0 && F % NWC == 0 && K % (2 * BK) == 0 && K > 0, "gemm_swiglu_w4: M % 256, F % 112, K % 128 (got ",
-              M, " ", F, " ", K, ")");
+  TORCH_CHECK(M % BM == 0 && F % NWC == 0 && K % (2 * BK) == 0 && K > 0, "gemm_swiglu_w4: M % 256, F % ", NWC,
+              ", K % 128 (got ", M, " ", F, " ", K, ")");
   TORCH_CHECK(M * K * 2 < (1L << 32) && F2 * K * 2 < (1L << 32), "gemm_swiglu_w4: operand over 4 GiB");
   const at::DeviceGuard guard(x.device());
   auto gu = at::empty({M, F2}, x.options());
@@ -437,6 +458,7 @@ at::Tensor gemm_swiglu_bwd_w4(const at::Tensor& dy, const at::Tensor& w2, const 
 }
 
 int64_t gemm_w4_pick(int64_t M, int64_t N) { return pick_nj(M, N); }
+int64_t gemm_swiglu_pick(int64_t M, int64_t F) { return pick_swiglu_nj(M, F); }
 
 // FT_W4_SPLITK at run time (A/B): 0 off, 1 automatic, 2 forced where it fits
 void gemm_w4_set_splitk(int64_t mode) { g_splitk_mode = (int)mode; }
@@ -505,6 +527,8 @@ TORCH_LIBRARY_FRAGMENT(ftamd, m) {
   m.def("gemm_qkv_rope_w4(Tensor x, Tensor w, Tensor cos, Tensor sin, int seq, int hq, int hkv, int d) -> Tensor",
         &gemm_qkv_rope_w4);
   m.def("gemm_w4_pick(int M, int N) -> int", &gemm_w4_pick);
-  m.def("gemm_swiglu_w4(Tensor x, Tensor w13, bool with_t=True) -> (Tensor, Tensor, Tensor)", &gemm_swiglu_w4);
+  m.def("gemm_swiglu_w4(Tensor x, Tensor w13, bool with_t=True, int nj=0) -> (Tensor, Tensor, Tensor)",
+        &gemm_swiglu_w4);
+  m.def("gemm_swiglu_pick(int M, int F) -> int", &gemm_swiglu_pick);
   m.def("gemm_swiglu_bwd_w4(Tensor dy, Tensor w2, Tensor gu, int nj=0) -> Tensor", &gemm_swiglu_bwd_w4);
 }

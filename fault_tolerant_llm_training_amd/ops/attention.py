@@ -165,7 +165,8 @@ def rope_attention(qkv, cos, sin, seq_len, hq, hkv, d, keep: Optional[AttentionK
 # kernel alone runs the Llama-3-8B QKV shape at 1.10-1.14x hipBLASLt, profiles/r3_gemm_w4_investigation.md);
 # set_qkv_rope(False) restores the plain projection + the RoPE kernel (A/B).
 _QKV_ROPE = True
-_QKV_ROPE_MIN_K = 2048  # model dim from which the fused projection wins (see _qkv_rope_ok)
+# model dim from which the fused projection wins (see _qkv_rope_ok; FT_QKV_ROPE_MIN_K: A/B)
+_QKV_ROPE_MIN_K = int(os.environ.get("FT_QKV_ROPE_MIN_K", "2048"))
 
 
 def set_qkv_rope(on: bool) -> None:

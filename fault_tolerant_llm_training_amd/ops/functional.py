@@ -2,11 +2,14 @@
 
 GPU tensors run the hand-written gfx950 kernels in ``csrc/kernels`` (loaded by
 :func:`fault_tolerant_llm_training_amd._native.kernels`, which raises if the
-library is missing) and hipBLASLt GEMMs through ``torch.mm``/``torch.addmm``.
+library is missing). Every bf16 / fp16 GEMM of the Llama-3-8B and GPT-2 presets runs on the
+hand-written w4 MFMA kernel (``csrc/kernels/gemm_w4.h``; the routing table per preset is pinned by
+``tests/test_routing_cpu.py``); hipBLASLt (``torch.mm`` / ``torch.addmm``) remains for the fp32 /
+fp64 models (the MFMA kernels are 16-bit: ``--model-dtype fp32`` logs that fallback once at
+startup) and for shapes no w4 tile fits.
 Model dtypes (``--model-dtype``): bf16 (every kernel), fp16 (every kernel; the MFMA GEMM and
 flash kernels in their fp16 variants), fp32 (the element-wise / reduction kernels in fp32,
-fp32 attention kernels, fp32 hipBLASLt GEMMs; the bf16-only paths — the round-2 hand GEMM, the
-transpose-based weight gradients, the fused SwiGLU transposes — route by dtype).
+fp32 attention kernels, fp32 hipBLASLt GEMMs).
 CPU tensors run a pure-PyTorch reference of the same math (the CPU backend for
 the gloo tests); its backward recomputes the forward under autograd.
 
@@ -37,11 +40,12 @@ IGNORE_INDEX = -100
 # GEMM routing. Every product of the step runs on the hand-written gfx950 "w4" kernel
 # (csrc/kernels/gemm_w4.h) on its operands as stored -- forward x W^T (K-contiguous), dX = dY W
 # (k-major W), dW = dY^T X (k-major dY and X, into the flat gradient buffer with the gradient-norm
-# partials in the epilogue) -- whenever its tile plan (tile width, split-K) fills at least half of
-# the 256 CUs. Smaller products (the GPT-2-sized projections at one sequence per GPU) are
-# latency-bound and go to hipBLASLt (torch.mm), or, opt-in, to the 128 x 128-tile kernel
-# (gemm_s.hip, set_gemm_s). Per-product plans and measurements: profiles/r5_w4_split_bench.log,
-# profiles/r4_gemm_w4t_bench.log; the routing table per preset: tests/test_routing_cpu.py.
+# partials in the epilogue). The GPT-2-sized products (18-96 tiles at one sequence per GPU) take a
+# deterministic K split (the dW layout too since round 6) and, for the LM-head dW at V = 50304, a
+# tail tile (M % 256). Per-product plans and measurements: profiles/r6/gpt2_gemm_probe_*.log,
+# profiles/r5_w4_split_bench.log; the routing table per preset: tests/test_routing_cpu.py.
+# set_w4_small(False) (FT_W4_SMALL=0) restores the round-5 routing of the small products to
+# hipBLASLt (A/B); the 128 x 128-tile kernel (gemm_s.hip, set_gemm_s) is opt-in.
 # ---------------------------------------------------------------------------------------------
 # FT_GEMM_BLAS=1: every GEMM on hipBLASLt (and the separate RoPE / SwiGLU kernels): the plain
 # reference path of convergence comparisons (scripts/gpu_convergence.sh)
@@ -54,6 +58,13 @@ _W4_DTYPES = (torch.bfloat16, torch.float16)  # bf16 / fp16 MFMA variants of the
 _W4_MIN_TILES = 128
 _W4_SHORT_K = 1024
 _W4_DEEP_K = 4096
+_W4_SMALL = os.environ.get("FT_W4_SMALL", "1") != "0"  # round 6: the GPT-2-sized products on w4 too
+_W4_SMALL_WGS = 16  # ... from this many workgroups (the GPT-2-small wo dW: 18 tiles x 3 slices)
+
+
+def set_w4_small(on: bool) -> None:
+    global _W4_SMALL
+    _W4_SMALL = bool(on)
 
 
 def set_w4_fwd(on: bool) -> None:
@@ -80,17 +91,21 @@ def set_w4_splitk(mode: int) -> None:
 
 
 def w4_route(M: int, N: int, K: int, a_t: bool, b_t: bool, *ts) -> bool:
-    """C[M, N] over a K-deep sum on the w4 kernel? 16-bit CUDA operands of one dtype, M % 256,
-    K % 128, a tile width for N, and a plan of at least _W4_MIN_TILES workgroups."""
+    """C[M, N] over a K-deep sum on the w4 kernel? 16-bit CUDA operands of one dtype, M % 256 (the
+    dW layout: M % 8, a tail tile), K % 128, a tile width for N, and a plan of enough workgroups."""
     if _BLAS_ONLY or not (all(t.is_cuda and t.dtype in _W4_DTYPES for t in ts) and len({t.dtype for t in ts}) == 1):
         return False
-    if M % 256 or K % 128 or K < 128:  # K-tiles of 64 in pairs
+    if (M % 256 and not (a_t and M % 8 == 0)) or K % 128 or K < 128:  # K-tiles of 64 in pairs
         return False
     nj, splits = _w4_plan(M, N, K, a_t, b_t)
     if nj == 0:
         return False
-    wgs = (M // 256) * (N // (32 * nj)) * splits
-    if a_t:  # dW: no split on this layout
+    wgs = -(-M // 256) * (N // (32 * nj)) * splits
+    if _W4_SMALL:
+        return wgs >= min(_W4_MIN_TILES, _W4_SMALL_WGS)
+    if M % 256:
+        return False
+    if a_t:  # dW (round 5: never split)
         return wgs >= _W4_MIN_TILES
     # forward / dX below a full round (GPT-2 sizes, profiles/r5_gpt2_gemm_probe.log): short
     # reductions (K <= 1024: wo forward / dX on 48-64 tiles, 1.15-1.39x hipBLASLt) and deep
@@ -126,12 +141,14 @@ _W4_WIDE_MIN_K = 2048
 
 
 def _w4_fwd_ok(T: int, N: int, K: int, x2, w) -> bool:
-    """The forward product on w4; the 256-wide tile below K = 2048 only within one round (the
-    GPT-2-medium w1|w3: 176 tiles, 27.7 vs 35.0 us for hipBLASLt)."""
+    """The forward product on w4; before round 6 the 256-wide tile below K = 2048 only within one
+    round (the GPT-2-medium w1|w3: 176 tiles, 27.7 vs 35.0 us for hipBLASLt). Since round 6
+    (_W4_SMALL) the GPT-2 LM head at V = 131072, K = 768 / 1024 runs on it too: 0.79x hipBLASLt
+    there, the 128-wide tile 0.60x (profiles/r6/gpt2_gemm_probe_small.log)."""
     if not (_W4_FWD and w.is_contiguous() and w4_route(T, N, K, False, False, x2, w)):
         return False
     nj, sp = _w4_plan(T, N, K, False, False)
-    return K >= _W4_WIDE_MIN_K or nj <= 6 or (T // 256) * (N // (32 * nj)) * sp <= 256
+    return _W4_SMALL or K >= _W4_WIDE_MIN_K or nj <= 6 or (T // 256) * (N // (32 * nj)) * sp <= 256
 
 
 def mm_fwd(x2: torch.Tensor, w: torch.Tensor, residual: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -513,17 +530,27 @@ def set_w4_swiglu(on: bool) -> None:
 
 def _ffn_w4t_ok(x2: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor) -> bool:
     """Every FFN product on the w4 kernel with no transposed operand anywhere: forward w1|w3 with the
-    SwiGLU epilogue (F % 112, no K split: its tile grid must fill half the chip), backward da on
-    k-major w2 with the SwiGLU-backward epilogue, dW2 / dW13 on k-major dY and activations, dX on
-    k-major w13 (bf16 or fp16)."""
+    SwiGLU epilogue (a tile width of 16 NJ features for F, no K split: gemm_swiglu_pick; the 8B F =
+    14336 at 112 features, GPT-2 at 64 / 128), backward da on k-major w2 with the SwiGLU-backward
+    epilogue, dW2 / dW13 on k-major dY and activations, dX on k-major w13 (bf16 or fp16)."""
     if not (_W4_SWIGLU and _W4_FWD and _W4_BWD and w13.is_contiguous() and w2.is_contiguous()):
         return False
     T, D = x2.shape
     F = w2.shape[1]
-    if T % 256 or D % 128 or F % 112 or (T // 256) * (F // 112) < _W4_MIN_TILES:
+    if T % 256 or D % 128:
+        return False
+    nj = _swiglu_nj(T, F)
+    if nj == 0 or (T // 256) * (F // (16 * nj)) < (min(_W4_MIN_TILES, _W4_SMALL_WGS) if _W4_SMALL else _W4_MIN_TILES):
+        return False
+    if not _W4_SMALL and F % 112:
         return False
     return (w4_route(T, F, D, False, True, x2, w2) and w4_route(2 * F, D, T, True, True, x2, w13)
             and w4_route(D, F, T, True, True, x2, w2) and w4_route(T, D, 2 * F, False, True, x2, w13))
+
+
+@functools.lru_cache(maxsize=64)
+def _swiglu_nj(T: int, F: int) -> int:
+    return int(kernels().gemm_swiglu_pick(T, F))
 
 
 class FeedForwardW4Fn(torch.autograd.Function):

@@ -221,6 +221,11 @@ def train(args) -> int:
         # gfx950 kernels cover bf16 / fp16 / fp32, so fp64 tensors take the composed-PyTorch path
         # (rocBLAS dgemm, reference attention): correct, not fast
         logger.info("--model-dtype fp64 on the GPU: composed PyTorch ops (the HIP kernels cover bf16/fp16/fp32)")
+    if model_dtype == torch.float32:
+        # the reference accepts fp32 (utils.py:14-19); the hand-written MFMA GEMM is 16-bit, so an
+        # fp32 model's GEMMs are the vendor's (ops/functional.py routing; tests/test_routing_cpu.py)
+        logger.info("--model-dtype fp32: GEMMs on hipBLASLt (torch.mm) -- the hand-written w4 MFMA GEMM is "
+                    "bf16/fp16; norms, RoPE, SwiGLU, attention, cross-entropy and AdamW keep their fp32 HIP kernels")
     torch.manual_seed(args.seed)
     from .ops.attention import set_deterministic
 

@@ -62,7 +62,7 @@ def main():
                 continue
             tiles = ((M + 255) // 256) * (N // (32 * nj))
             for sp in ((1,) if big else (1, 2, 3, 4, 6, 8)):
-                if Kd // 128 < sp or tiles * sp > 512 or (lay == "dw" and sp > 1 and nj != 4):
+                if Kd // 128 < sp or (tiles * sp > 512 and sp > 1) or (lay == "dw" and sp > 1 and nj != 4):
                     continue
                 cells.append((timeit(lambda: w4(nj, sp)), nj, sp, tiles * sp))
         best = min(cells)

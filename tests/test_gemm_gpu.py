@@ -138,7 +138,8 @@ def test_gemm_s_fp16():
     assert ((out.float() - ref).norm() / ref.norm()).item() < 2e-3
 
 
-@pytest.mark.parametrize("M,F,K", [(256, 448, 128), (512, 1792, 768), (2048, 14336, 4096)])
+@pytest.mark.parametrize("M,F,K", [(256, 448, 128), (512, 1792, 768), (2048, 14336, 4096), (2048, 2048, 768),
+                                   (2048, 2816, 1024)])
 def test_gemm_swiglu_w4(M, F, K):
     """w1|w3 GEMM with SwiGLU in the epilogue: gu equals the plain w4 GEMM bitwise (same MFMA order),
     a equals the SwiGLU kernel on that gu bitwise and a^T its transpose, and all match fp32
@@ -150,7 +151,8 @@ def test_gemm_swiglu_w4(M, F, K):
     x = (torch.rand(M, K, device="cuda") * 2 - 1).bfloat16()
     w13 = ((torch.rand(2 * F, K, device="cuda") * 2 - 1) * (1.0 / K**0.5)).bfloat16()
     gu, a, aT = K_.gemm_swiglu_w4(x, w13)
-    assert torch.equal(gu, K_.gemm_nt_w4(x, w13, None, None, 7))
+    nj = K_.gemm_swiglu_pick(M, F)  # 7 for the 8B F = 14336; 4 / 8 for GPT-2's 2048 / 2816
+    assert torch.equal(gu, K_.gemm_nt_w4(x, w13, None, None, nj))
     assert torch.equal(a, K_.swiglu_fwd(gu)) and torch.equal(aT, a.t().contiguous())
     ref = x.float() @ w13.float().t()
     g, u = ref[:, :F], ref[:, F:]

@@ -204,38 +204,38 @@ def test_split_k_8b_head_dx_vs_fp32():
 
 
 @pytest.mark.parametrize("M", [768, 1160, 50304])
-@pytest.mark.parametrize("splits", [1, 2, 3, 4])
-def test_dw_split_k_and_tail_tile(M, splits):
+@pytest.mark.parametrize("nj,splits", [(4, 1), (4, 2), (4, 3), (4, 4), (8, 1), (6, 1)])
+def test_dw_split_k_and_tail_tile(M, nj, splits):
     """The dW layout (k-major A and B) split over K (the GPT-2-sized weight gradients: 18-96 tiles of
     256 x 128 at 2048 tokens) and with a tail tile (M % 256 != 0: the GPT-2 LM-head dW at V = 50304):
     exact on integer operands for every split, the rows past M untouched, the sum-of-squares partials
     of the stored values only, the accumulate epilogue, and fp32-close on random operands."""
     k = K()
-    torch.manual_seed(M + splits)
+    torch.manual_seed(M + splits + nj)
     N, T = 768, 2048
     if M == 50304 and splits not in (1, 3):
         pytest.skip("the 50304 tail at two splits is enough")
     at = ints(T, M) + (torch.arange(M, device="cuda") % 3).bfloat16()  # dY [T, M] read k-major
     b = ints(T, N)
     ref = at.float().t() @ b.float()
-    tiles = ((M + 255) // 256) * (N // 128)
+    tiles = ((M + 255) // 256) * (N // (32 * nj))
     part = torch.full((tiles + 5,), 7.0, device="cuda")  # slots past the grid are zeroed
     big = torch.full((M + 64, N), 3.0, dtype=torch.bfloat16, device="cuda")  # rows past M: canary
     out = big[:M]
-    k.gemm_w4_ex(at, True, b, True, M, N, T, out, False, part, 4, splits)
+    k.gemm_w4_ex(at, True, b, True, M, N, T, out, False, part, nj, splits)
     assert torch.equal(out.float(), ref.bfloat16().float())
     assert (big[M:] == 3.0).all()
     assert part[tiles:].abs().sum().item() == 0
     sq = (out.float() ** 2).sum().item()
     assert abs(part.sum().item() - sq) <= 1e-5 * sq
-    k.gemm_w4_ex(at, True, b, True, M, N, T, out, True, None, 4, splits)  # accumulate
+    k.gemm_w4_ex(at, True, b, True, M, N, T, out, True, None, nj, splits)  # accumulate
     assert torch.equal(out.float(), (2 * ref).bfloat16().float())
     # random operands: fp32-close, bitwise reproducible, and split == unsplit within rounding
     at.copy_(rnd(T, M))
     b.copy_(rnd(T, N))
     ref = at.float().t() @ b.float()
-    o1 = k.gemm_w4_ex(at, True, b, True, M, N, T, None, False, None, 4, splits)
-    o2 = k.gemm_w4_ex(at, True, b, True, M, N, T, None, False, None, 4, splits)
+    o1 = k.gemm_w4_ex(at, True, b, True, M, N, T, None, False, None, nj, splits)
+    o2 = k.gemm_w4_ex(at, True, b, True, M, N, T, None, False, None, nj, splits)
     assert rel(o1, ref) < 4e-3 and torch.equal(o1, o2)
 
 

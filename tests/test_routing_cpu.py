@@ -5,8 +5,8 @@ each product of the step takes, so a routing change is a visible test change:
 * Llama-3-8B bf16 / fp16: every product on the hand-written w4 kernel -- none on hipBLASLt (the
   deep-reduction dX products with a K split);
 * fp32 models and CPU tensors: hipBLASLt / the composed path (the MFMA kernels are 16-bit);
-* GPT-2-sized presets at one sequence: the products whose w4 plan fills half the chip on w4,
-  the rest (latency-bound) on hipBLASLt.
+* GPT-2-sized presets at one sequence: every product on w4 too (round 6: K splits for the small
+  grids, a tail tile for V % 256), none on hipBLASLt.
 """
 import pytest
 import torch
@@ -42,18 +42,28 @@ def test_fp32_and_cpu_take_no_mfma_gemm(preset):
 @pytest.mark.parametrize("preset,vocab", [("gpt2-small", 50304), ("gpt2-small", 131072),
                                           ("gpt2-medium", 50304), ("gpt2-medium", 131072)])
 def test_gpt2_routes(preset, vocab):
+    """Round 6: no GPT-2 product on hipBLASLt. The 18-96-tile weight gradients take a K split (the
+    dW layout splits its 128-wide tile), the 2048-3072-deep forward / dX products too, the FFN runs
+    fused (SwiGLU in the w1|w3 epilogue, its backward in the w2 dX epilogue), the LM-head dW at the
+    padded V = 50304 a tail tile, the V = 131072 logits the 256-wide tile (K = 768 / 1024)."""
     t = routing_table(model_args_for(preset, vocab_size=vocab, seq_len=2048), torch.bfloat16)
-    on_w4 = sorted(k for k, v in t.items() if v.startswith("w4"))
-    # the LM-head dX (K = V) always takes a K split on w4; the 768 / 1024-wide projections'
-    # forward / dX with enough tiles do too; wo (2048 x D x D, K = D <= 1024) runs its 48-64 tiles
-    # on w4 without a split (short reductions, profiles/r5_gpt2_gemm_probe.log), its dW (k-major A,
-    # K = 2048 tokens) stays on hipBLASLt
+    assert sorted(t) == sorted(PRODUCTS)
+    assert "hipBLASLt" not in t.values(), t
     assert t["head dX"].startswith("w4") and " x" in t["head dX"]
-    assert t["wo fwd"] == t["wo dX"] == "w4 128" and t["wo dW"] == "hipBLASLt"
-    assert t["qkv fwd"].startswith("w4") and t["w13 dX"].startswith("w4")
-    # the head's dW needs V % 256 (rows of the k-major tiles): GPT-2's padded 50304 stays on hipBLASLt
-    assert t["head dW"] == ("w4 256" if vocab % 256 == 0 else "hipBLASLt")
-    assert len(on_w4) >= 5, t
+    assert t["wo fwd"] == t["wo dX"] == "w4 128"
+    for k in ("qkv dW", "wo dW", "w2 dW", "w2 fwd", "qkv dX"):
+        assert " x" in t[k], (k, t[k])
+    assert t["w13 fwd"] == "w4 swiglu" and t["w2 dX"] == "w4 swiglu-bwd"
+    assert t["head dW"].startswith("w4")
+    if vocab == 131072:
+        assert t["head fwd"] == "w4 256"
+
+
+def test_gpt2_round5_routing_knob(monkeypatch):
+    """set_w4_small(False) (FT_W4_SMALL=0): the round-5 routing of the small products (A/B)."""
+    monkeypatch.setattr(Fx, "_W4_SMALL", False)
+    t = routing_table(model_args_for("gpt2-small", vocab_size=50304, seq_len=2048), torch.bfloat16)
+    assert t["wo dW"] == t["head dW"] == "hipBLASLt" and t["wo fwd"] == "w4 128"
 
 
 def test_blas_only_knob(monkeypatch):
@@ -63,3 +73,22 @@ def test_blas_only_knob(monkeypatch):
     t = routing_table(model_args_for("llama3-8b", vocab_size=131072, seq_len=2048), torch.bfloat16)
     assert set(t.values()) == {"hipBLASLt"}
     assert A._qkv_rope_ok is not None
+
+
+def test_fp32_model_logs_the_hipblaslt_fallback_once(tmp_path):
+    """--model-dtype fp32 (reference utils.py:14-19): the hand-written MFMA GEMM is 16-bit, so the
+    GEMMs of an fp32 model are hipBLASLt's -- a documented deviation, logged once at startup, never
+    silent."""
+    import os
+
+    from helpers import TINY, run_train, write_fake_sbatch
+
+    d = str(tmp_path)
+    write_fake_sbatch(d)
+    rc, out = run_train(d, "4101", TINY + ["--synthetic-data", "--vocab-size", "256", "--model-dtype", "fp32",
+                                           "--training-steps", "3", "--checkpoint-path", os.path.join(d, "ck")])
+    assert rc == 0 and "Training completed" in out, out[-2000:]
+    assert out.count("--model-dtype fp32: GEMMs on hipBLASLt") == 1, out[-2000:]
+    rc, out = run_train(d, "4102", TINY + ["--synthetic-data", "--vocab-size", "256", "--training-steps", "2",
+                                           "--checkpoint-path", os.path.join(d, "ck")])
+    assert rc == 0 and "GEMMs on hipBLASLt" not in out
