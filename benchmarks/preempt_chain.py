@@ -85,13 +85,22 @@ def main():
                          "that holds ONE checkpoint, e.g. 79 GB for the 48 GB 8B file: the next save "
                          "needs the space; a job that dies before its own save then has nothing to "
                          "resume from -- the trade --prune-consumed avoids where two fit)")
+    ap.add_argument("--rotate", default="",
+                    help="a second checkpoint directory (another filesystem): train.py --checkpoint-alt-path DIR "
+                         "--prune-consumed -- each job writes to the directory it did not resume from and "
+                         "deletes its predecessor's file only once its own is durable, so a disk with room for "
+                         "ONE checkpoint still always holds a complete one (the other tier holds the other)")
     ap.add_argument("train_args", nargs=argparse.REMAINDER)
     a = ap.parse_args()
     extra = [x for x in a.train_args if x != "--"]
     ck = a.checkpoint_path or tempfile.mkdtemp(prefix="ftck_")
+    dirs = [ck] + ([a.rotate] if a.rotate else [])
+    for d_ in dirs:
+        os.makedirs(d_, exist_ok=True)
     env = dict(os.environ)
+    rot = ["--checkpoint-alt-path", a.rotate, "--prune-consumed"] if a.rotate else []
     env["EXTRA_TRAINING_ARGS"] = " ".join(extra + ["--training-steps", "100000000", "--error-step", "100000000",
-                                                   "--checkpoint-path", ck])
+                                                   "--checkpoint-path", ck] + rot)
     env.setdefault("PYTHONUNBUFFERED", "1")
     logdir = a.log_dir or tempfile.mkdtemp(prefix="ftlogs_")
     os.makedirs(logdir, exist_ok=True)
@@ -120,7 +129,29 @@ def main():
                 os.remove(path)
             pruned.append(prev)
 
-    jobs = sim.run(a.jobs, prune if (a.prune_consumed or a.prune_on_resume) else None)
+    # complete checkpoint files (atomically renamed *.ckpt) over every directory, sampled every poll
+    # (50 ms) while a job runs: after the first one exists the chain must never hold zero
+    durable = {"min": None, "max": 0, "samples": 0}
+
+    def count_durable():
+        n = 0
+        for d_ in dirs:
+            try:
+                n += sum(1 for f in os.listdir(d_) if f.startswith("checkpoint_") and f.endswith(".ckpt"))
+            except OSError:
+                pass
+        durable["max"] = max(durable["max"], n)
+        if n or durable["min"] is not None:
+            durable["min"] = n if durable["min"] is None else min(durable["min"], n)
+            durable["samples"] += 1
+
+    def hook(rec):
+        if a.prune_consumed or a.prune_on_resume:
+            prune(rec)
+        count_durable()
+
+    jobs = sim.run(a.jobs, hook)
+    count_durable()
     rows, lost = [], 0
     prev = None
     for j in jobs:
@@ -133,6 +164,10 @@ def main():
     print(json.dumps({"benchmark": "preempt_chain", "args": extra, "time_limit_s": a.time,
                       "signal_lead_s": a.signal_lead, "jobs": rows, "steps_lost": lost,
                       "pruned_checkpoints": pruned,
+                      "checkpoint_dirs": dirs,
+                      "final_checkpoints": {d_: sorted(os.listdir(d_)) for d_ in dirs},
+                      "durable_checkpoints_min_after_first": durable["min"],
+                      "durable_checkpoints_max": durable["max"], "durable_samples": durable["samples"],
                       "logs": logdir}), flush=True)
     return 0
 

@@ -72,13 +72,18 @@ Plan pick_plan(long M, long N, long K, bool kmajor_a, bool kmajor_b) {
   const long tm = (M + BM - 1) / BM, nkt = K / BK;
   Plan best{pick_nj(M, N, kmajor_a), 1};
   if (g_splitk_mode == 0 || best.nj == 0) return best;
-  // per slice: its K-tiles, the epilogue (~3 K-tiles), the partial's store (~3) and, for the last
-  // slice, reading the S - 1 partials (~3 each)
+  // per slice: its K-tiles, the epilogue (~3 K-tiles) and ~6 K-tiles per slice for the hand-off
+  // (the partial's fp32 store, the flag, the last slice's reads): fitted to the GPT-2 products,
+  // t(S) ~ a + b K/S + c S with c / b ~ 6 K-tiles (profiles/r6/gpt2_gemm_probe_*.log: the
+  // GPT-2-small w1|w3 dX at S = 1 / 2 / 3 / 4: 49.7 / 35.0 / 31.9 / 32.9 us)
+  // (the 8B dX / w2 products, >= 128 tiles, keep the round-5 constant of 3: their plans were
+  // measured there, profiles/r5_w4_split_bench.log)
   auto cost = [&](int nj, int sp) {
     const long tiles = tm * (N / (32L * nj));
     const long rounds = (tiles * sp + 255) / 256;
     const double eff = nj == 8 ? 1.0 : nj == 7 ? 0.99 : nj == 6 ? 0.98 : (kmajor_a ? 0.65 : kmajor_b ? 0.85 : 0.92);
-    return (double)rounds * nj * ((double)nkt / sp + 3.0 + (sp > 1 ? 3.0 * sp : 0.0)) / eff;
+    const double hand = tm * (N / 256) >= 128 ? 3.0 : 6.0;
+    return (double)rounds * nj * ((double)nkt / sp + 3.0 + (sp > 1 ? hand * sp : 0.0)) / eff;
   };
   double bc = cost(best.nj, 1);
   for (int nj : {8, 7, 6, 4}) {

@@ -84,6 +84,12 @@ def _w4_plan(M: int, N: int, K: int, a_t: bool, b_t: bool):
     return tuple(kernels().gemm_w4_plan(M, N, K, a_t, b_t))
 
 
+def _w4_wgs(M: int, N: int, K: int, a_t: bool, b_t: bool) -> int:
+    """Workgroups of the w4 kernel's automatic plan for C[M, N] over K (0: no plan)."""
+    nj, sp = _w4_plan(M, N, K, a_t, b_t)
+    return -(-M // 256) * (N // (32 * nj)) * sp if nj else 0
+
+
 def set_w4_splitk(mode: int) -> None:
     """Split-K of the w4 kernel (FT_W4_SPLITK): 0 off, 1 automatic (default), 2 forced where it fits."""
     kernels().gemm_w4_set_splitk(int(mode))
@@ -247,7 +253,10 @@ def weight_grad_async(dy2: torch.Tensor, x2: torch.Tensor, sink: Optional[GradSi
         return weight_grad(dy2, x2, sink)
     dy2 = dy2.contiguous()
     x2 = x2.contiguous()
-    if not _W4_DW_SIDE and _w4_dw_ok(dy2.shape[0], dy2.shape[1], x2.shape[1], dy2, x2):
+    T, N, K = dy2.shape[0], dy2.shape[1], x2.shape[1]
+    if not _W4_DW_SIDE and _w4_dw_ok(T, N, K, dy2, x2) and _w4_wgs(N, K, T, True, True) >= 256:
+        # a full-chip w4 dW runs inline; the GPT-2-sized ones (54-192 workgroups) run on the side
+        # stream beside the dX product of the same node, which leaves the rest of the CUs idle too
         return weight_grad(dy2, x2, sink)
     # Operand lifetime is stream-ordered instead of record_stream(): the operands stay referenced in
     # a short FIFO; before one is dropped the compute stream waits for its dW, so the freed blocks

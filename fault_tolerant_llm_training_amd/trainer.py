@@ -233,9 +233,13 @@ def train(args) -> int:
     job_id = jobid()
 
     checkpoint = None
+    resume_file = None  # the file this job resumed from (--prune-consumed deletes it later)
     if args.checkpoint_id:
-        logger.info(f"Loading checkpoint from {args.checkpoint_path}")
-        checkpoint = load_checkpoint(checkpoint_file(args.checkpoint_path, args.checkpoint_id))
+        dirs = [args.checkpoint_path] + ([args.checkpoint_alt_path] if args.checkpoint_alt_path else [])
+        cands = [checkpoint_file(d_, args.checkpoint_id) for d_ in dirs]
+        resume_file = next((c for c in cands if os.path.exists(c)), cands[0])
+        logger.info(f"Loading checkpoint from {os.path.dirname(resume_file) or args.checkpoint_path}")
+        checkpoint = load_checkpoint(resume_file)
 
     logger.info("Setting up DataLoaders...")
     holder: Dict[str, Any] = {}
@@ -356,8 +360,28 @@ def train(args) -> int:
             raise RuntimeError(f"ranks disagree on training_step: {steps}")
         logger.info(f"Data parallel over {info.world_size} ranks: {reducer.summary()}")
 
-    ckpt_path = checkpoint_file(args.checkpoint_path, job_id)
+    save_dir = args.checkpoint_path
+    if args.checkpoint_alt_path and resume_file is not None and \
+            os.path.realpath(os.path.dirname(resume_file)) == os.path.realpath(args.checkpoint_path):
+        save_dir = args.checkpoint_alt_path  # rotate: never overwrite or crowd out the file resumed from
+    ckpt_path = checkpoint_file(save_dir, job_id)
+    if args.checkpoint_alt_path:
+        logger.info(f"Checkpoints of this job go to {save_dir}")
     ckpt = {"engine": None}
+
+    def prune_consumed() -> None:
+        """--prune-consumed: this job's own checkpoint is durable; the one it resumed from goes."""
+        nonlocal resume_file
+        if not (args.prune_consumed and info.is_main and resume_file is not None):
+            return
+        if os.path.realpath(resume_file) == os.path.realpath(ckpt_path):
+            return
+        try:
+            os.remove(resume_file)
+            logger.info(f"Deleted the consumed checkpoint {resume_file} (this job's {ckpt_path} is durable)")
+        except FileNotFoundError:
+            pass
+        resume_file = None
     # periodic saves: on by default under data parallelism (BASELINE config 3 cadence), so a
     # lost rank (OOM-kill, node failure) costs at most that many steps — ZeRO-1 survivors
     # cannot write its optimizer shards (reference train.py:121-129 saves on every path it sees)
@@ -562,6 +586,7 @@ def train(args) -> int:
                 if done is not None:
                     logger.info(f"Checkpoint written: {done.path} ({done.bytes / 1e9:.2f} GB, "
                                 f"stall {done.stall_s:.3f}s, durable after {done.total_s:.2f}s)")
+                    prune_consumed()
             except Exception as e:  # noqa: BLE001 - becomes this rank's vote for the error path
                 if pending_err is None:
                     pending_err = e
@@ -574,8 +599,10 @@ def train(args) -> int:
             if batch is None:  # unreachable: a local error always stops every rank above
                 raise RuntimeError("no batch")
             if save_due:
-                save_checkpoint(blocking=args.no_async_checkpoint, step_now=training_step)
+                st_ = save_checkpoint(blocking=args.no_async_checkpoint, step_now=training_step)
                 last_save_step = training_step
+                if args.no_async_checkpoint and st_ is not None:
+                    prune_consumed()
 
             if prof_range is not None and training_step == prof_range[0] and prof is None:
                 acts = [torch.profiler.ProfilerActivity.CPU]
@@ -717,6 +744,7 @@ def train(args) -> int:
                 logger.info(f"Checkpoint {st.path}: {st.bytes / 1e9:.2f} GB in {st.total_s:.2f}s "
                             f"(mode {st.mode})")
                 log_digest(step_now, " (saved)")
+                prune_consumed()
 
         if exit_type == -1 and not isinstance(e, InjectedFault) and info.is_main:
             logger.error(f"Training error: {e!r}")

@@ -145,6 +145,21 @@ def build_parser() -> argparse.ArgumentParser:
         "straight into pinned host memory; auto = hbm when free HBM allows",
     )
     parser.add_argument(
+        "--checkpoint-alt-path",
+        type=str,
+        default="",
+        help="A second checkpoint directory (another filesystem): a job that resumed from a file in one "
+        "of the two directories writes its own checkpoints to the other, so the file it resumed from "
+        "stays intact until its own is durable (a disk with room for ONE checkpoint, e.g. the 48 GB 8B "
+        "file on 79 GB). --checkpoint-id is looked up in both",
+    )
+    parser.add_argument(
+        "--prune-consumed",
+        action="store_true",
+        help="Delete the checkpoint this job resumed from once this job's own checkpoint is durable "
+        "(periodic or exit save): the chain keeps at least one complete checkpoint at every moment",
+    )
+    parser.add_argument(
         "--no-checkpoint-prealloc",
         action="store_true",
         help="Pin the checkpoint host buffers at the first save instead of in a background thread at startup",

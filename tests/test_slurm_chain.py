@@ -66,3 +66,35 @@ def test_preempt_chain_prunes_consumed_checkpoints(tmp_path, mode):
     assert res["steps_lost"] == 0 and all(j["saved_at"] for j in res["jobs"]), res
     assert res["pruned_checkpoints"] == ids[:2], res
     assert sorted(os.listdir(ck)) == [f"checkpoint_{ids[2]}.ckpt"]
+
+
+def test_preempt_chain_rotates_two_tiers_and_never_holds_zero_checkpoints(tmp_path):
+    """benchmarks/preempt_chain.py --rotate DIR2 (train.py --checkpoint-alt-path --prune-consumed): each
+    job resumes from one directory, writes its own checkpoint to the other, and deletes its
+    predecessor's file only once its own is durable. Sampled every 50 ms over the whole chain, the
+    two directories never hold zero complete checkpoints after the first save, and never more than
+    two; zero steps lost (the safe order on a disk with room for one 8B checkpoint: round-5 review)."""
+    import json
+    import subprocess
+    import sys
+
+    ck, alt = tmp_path / "disk", tmp_path / "shm"
+    env = dict(os.environ, OMP_NUM_THREADS="2", PYTHONUNBUFFERED="1")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "benchmarks", "preempt_chain.py"), "--jobs", "3",
+                        "--time", "14", "--signal-lead", "7", "--checkpoint-path", str(ck), "--rotate", str(alt),
+                        "--", "--device", "cpu", "--model", "tiny", "--synthetic-data", "--vocab-size", "256",
+                        "--sequence-length", "32", "--logging-frequency", "50"],
+                       env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    ids = [j["job"] for j in res["jobs"]]
+    assert res["steps_lost"] == 0 and all(j["saved_at"] for j in res["jobs"]), res
+    # (two coexist only between a job's save and its predecessor's deletion: a few ms, rarely sampled)
+    assert res["durable_checkpoints_min_after_first"] == 1 and res["durable_checkpoints_max"] in (1, 2), res
+    assert res["durable_samples"] > 50, res
+    # job 1 -> disk, job 2 (resumed from disk) -> shm, job 3 (resumed from shm) -> disk; predecessors gone
+    assert sorted(os.listdir(ck)) == [f"checkpoint_{ids[2]}.ckpt"] and os.listdir(alt) == [], res
+    logs = [open(os.path.join(res["logs"], f"output_{i}.out")).read() for i in ids]
+    assert f"Checkpoints of this job go to {alt}" in logs[1] and f"Checkpoints of this job go to {ck}" in logs[2]
+    assert f"Deleted the consumed checkpoint {ck}/checkpoint_{ids[0]}.ckpt" in logs[1]
+    assert f"Deleted the consumed checkpoint {alt}/checkpoint_{ids[1]}.ckpt" in logs[2]
