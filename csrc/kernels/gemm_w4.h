@@ -452,10 +452,11 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(W4Args p) {
 
   // LDS-DMA sources. Instruction q of wave w fills image piece P = q * 4 + w (bytes [P KiB, +1 KiB)),
   // lane L its 16 B at P KiB + 16 L; the lane's source is the element that image slot holds.
-  // A tail tile (M % 256: the GPT-2 LM-head dW, M = V = 50304) clamps the sources of its rows past M
-  // onto row M - 1 (K-contiguous A) / the last 8-row chunk (k-major A, M % 8): every load stays
-  // inside A, and those rows' results are never stored.
+  // A tail tile of the dW layout (M % 256: the GPT-2 LM-head dW, M = V = 50304) clamps the sources of
+  // its rows past M onto the last 8-row chunk (k-major A, M % 8): every load stays inside A, and
+  // those rows' results are never stored. (The other layouts take M % 256: no clamp, no guard.)
   const int mlast = min(BM, p.M - m0) - 1;  // last valid tile row
+  const bool mtail = AT && m0 + BM > p.M;   // uniform
   Ctx c;
   c.wid = wid;
   c.lds0 = __builtin_amdgcn_readfirstlane(lds_u32(smem));
@@ -476,7 +477,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(W4Args p) {
     c.srdA = make_srd(p.a + (long)m0 * p.lda + k0);
     c.stepA = (unsigned)(BK * 2);
 #pragma unroll
-    for (int q = 0; q < 8; ++q) c.voA[q] = (unsigned)((min(q * 32 + lrow, mlast) * p.lda + lch * 8) * 2);
+    for (int q = 0; q < 8; ++q) c.voA[q] = (unsigned)(((q * 32 + lrow) * p.lda + lch * 8) * 2);
   }
   if constexpr (BT) {
     c.srdB = make_srd(p.b + n0 + k0 * p.ldb);
@@ -757,51 +758,62 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(W4Args p) {
       }
     }
   } else if (cc < 2 * NJ) {
+    // the store loop in two copies: a tail tile's guards rows past M (not stored, nor summed), every
+    // other tile runs without the per-row compare (mtail is uniform; only the dW layout has tails)
+    auto store_rows = [&](auto tail_tag) {
+      constexpr bool TAIL = decltype(tail_tag)::value;
 #pragma unroll 4
-    for (int rr = 0; rr < 32; ++rr) {
-      const int row = rr * 4 + (lane >> 4);
-      const long gm = m0 + wm * 128 + row;
-      if (gm >= p.M) continue;  // tail tile: rows past M are not stored (nor summed)
-      uint4 v = *reinterpret_cast<const uint4*>(wl + row * 256 + ((cc ^ (row & 15)) << 4));
-      // W4_SWIGLU: wave column half 0 holds g (gu columns [0, F)), half 1 holds u ([F, 2F))
-      const int gn = EPI == W4_SWIGLU ? (wn ? p.ffn : 0) + f0 + cc * 8 : n0 + wn * NW + cc * 8;
-      if constexpr (EPI == W4_RES) {
-        float a[8], r[8];
-        unpack8e<E>(v, a);
-        unpack8e<E>(*reinterpret_cast<const uint4*>(p.r + gm * p.ldr + gn), r);
+      for (int rr = 0; rr < 32; ++rr) {
+        const int row = rr * 4 + (lane >> 4);
+        const long gm = m0 + wm * 128 + row;
+        if constexpr (TAIL) {
+          if (gm >= p.M) continue;
+        }
+        uint4 v = *reinterpret_cast<const uint4*>(wl + row * 256 + ((cc ^ (row & 15)) << 4));
+        // W4_SWIGLU: wave column half 0 holds g (gu columns [0, F)), half 1 holds u ([F, 2F))
+        const int gn = EPI == W4_SWIGLU ? (wn ? p.ffn : 0) + f0 + cc * 8 : n0 + wn * NW + cc * 8;
+        if constexpr (EPI == W4_RES) {
+          float a[8], r[8];
+          unpack8e<E>(v, a);
+          unpack8e<E>(*reinterpret_cast<const uint4*>(p.r + gm * p.ldr + gn), r);
 #pragma unroll
-        for (int q = 0; q < 8; ++q) a[q] += r[q];
-        v = pack8e<E>(a);
-      } else if constexpr (EPI == W4_ROPE) {
-        if (gn < p.rope_cols) {
-          // 8 columns = 4 interleaved (x0, x1) pairs of one head: rotated in fp32 by the bf16
-          // projection output, as the separate kernel did (rope.hip / model.py:121-126)
-          const int pos = (int)(gm % p.rope_seq);
-          const int i0 = (gn % p.rope_hd) >> 1;
-          const float* cs = p.cos_t + (long)pos * (p.rope_hd >> 1) + i0;
-          const float* sn = p.sin_t + (long)pos * (p.rope_hd >> 1) + i0;
-          const float4 c4 = *reinterpret_cast<const float4*>(cs);
-          const float4 s4 = *reinterpret_cast<const float4*>(sn);
+          for (int q = 0; q < 8; ++q) a[q] += r[q];
+          v = pack8e<E>(a);
+        } else if constexpr (EPI == W4_ROPE) {
+          if (gn < p.rope_cols) {
+            // 8 columns = 4 interleaved (x0, x1) pairs of one head: rotated in fp32 by the bf16
+            // projection output, as the separate kernel did (rope.hip / model.py:121-126)
+            const int pos = (int)(gm % p.rope_seq);
+            const int i0 = (gn % p.rope_hd) >> 1;
+            const float* cs = p.cos_t + (long)pos * (p.rope_hd >> 1) + i0;
+            const float* sn = p.sin_t + (long)pos * (p.rope_hd >> 1) + i0;
+            const float4 c4 = *reinterpret_cast<const float4*>(cs);
+            const float4 s4 = *reinterpret_cast<const float4*>(sn);
+            float a[8];
+            unpack8e<E>(v, a);
+            const float cv[4] = {c4.x, c4.y, c4.z, c4.w}, sv[4] = {s4.x, s4.y, s4.z, s4.w};
+            float o[8];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              o[2 * q] = a[2 * q] * cv[q] - a[2 * q + 1] * sv[q];
+              o[2 * q + 1] = a[2 * q] * sv[q] + a[2 * q + 1] * cv[q];
+            }
+            v = pack8e<E>(o);
+          }
+        }
+        if (p.part != nullptr) {
           float a[8];
           unpack8e<E>(v, a);
-          const float cv[4] = {c4.x, c4.y, c4.z, c4.w}, sv[4] = {s4.x, s4.y, s4.z, s4.w};
-          float o[8];
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            o[2 * q] = a[2 * q] * cv[q] - a[2 * q + 1] * sv[q];
-            o[2 * q + 1] = a[2 * q] * sv[q] + a[2 * q + 1] * cv[q];
-          }
-          v = pack8e<E>(o);
+          for (int q = 0; q < 8; ++q) sq = fmaf(a[q], a[q], sq);
         }
+        if (!(p.dbg & 1)) *reinterpret_cast<uint4*>(p.c + gm * p.ldc + gn) = v;
       }
-      if (p.part != nullptr) {
-        float a[8];
-        unpack8e<E>(v, a);
-#pragma unroll
-        for (int q = 0; q < 8; ++q) sq = fmaf(a[q], a[q], sq);
-      }
-      if (!(p.dbg & 1)) *reinterpret_cast<uint4*>(p.c + gm * p.ldc + gn) = v;
-    }
+    };
+    if (mtail)
+      store_rows(std::true_type{});
+    else
+      store_rows(std::false_type{});
   }
   if (p.part != nullptr) {  // uniform: one partial per tile, fixed order (deterministic)
     sq = wave_sum(sq);

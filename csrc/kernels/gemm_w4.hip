@@ -257,8 +257,8 @@ at::Tensor gemm_w4_ex(const at::Tensor& a, bool a_t, const at::Tensor& b, bool b
   TORCH_CHECK(NJ == 8 || NJ == 7 || NJ == 6 || NJ == 4, "gemm_w4_ex: no tile width fits N = ", N);
   // M % 256 != 0 runs a tail tile (its rows past M clamped on load, not stored): the GPT-2 LM-head
   // dW at V = 50304 (k-major A reads 8-row chunks: M % 8)
-  TORCH_CHECK(M % 8 == 0 && M > 0 && N % (32 * NJ) == 0 && K % (2 * BK) == 0 && K > 0, "gemm_w4_ex: M % 8, N % ",
-              32 * NJ, ", K % 128 (got ", M, " ", N, " ", K, ")");
+  TORCH_CHECK((a_t ? M % 8 : M % BM) == 0 && M > 0 && N % (32 * NJ) == 0 && K % (2 * BK) == 0 && K > 0,
+              "gemm_w4_ex: M % ", a_t ? 8 : BM, ", N % ", 32 * NJ, ", K % 128 (got ", M, " ", N, " ", K, ")");
   // 32-bit buffer offsets: the whole operand (a K-tile advance is a scalar offset) under 4 GiB
   TORCH_CHECK(M * K * 2 < (1L << 32) && N * K * 2 < (1L << 32), "gemm_w4_ex: operand over 4 GiB");
   const at::DeviceGuard guard(a.device());

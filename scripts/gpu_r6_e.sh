@@ -4,13 +4,14 @@
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out
 R=$GRAFT_REPO_ROOT
 j() { python -c "import json,sys; d=json.loads(open('$1').read().strip().splitlines()[-1]); print(d['ms_per_step'], d.get('sclk_mhz_p50'), d.get('power_w_p50'))"; }
-for m in gpt2-small gpt2-medium; do for r in 1 2; do for v in r5 head head_w4small0; do
+for m in gpt2-small gpt2-medium; do for r in 1 2; do for v in r5 head head_w4small0 head_qkvrope; do
   if [ $v = r5 ]; then cd $R/abtree_r5; else cd $R; fi
   if [ $v = head_w4small0 ]; then export FT_W4_SMALL=0; else unset FT_W4_SMALL; fi
+  if [ $v = head_qkvrope ]; then export FT_QKV_ROPE_MIN_K=768; else unset FT_QKV_ROPE_MIN_K; fi
   timeout -k 10 300 python -u bench.py --model $m --vocab-size 50304 --graph --steps 50 --warmup 5 --no-ckpt > $R/gpurun_out/r6e_${m}_${v}_$r.log 2>&1 || exit 1
   echo "$m $v $r $(j $R/gpurun_out/r6e_${m}_${v}_$r.log)"
 done; done; done
-unset FT_W4_SMALL
+unset FT_W4_SMALL FT_QKV_ROPE_MIN_K
 for v in r5 head; do
   if [ $v = r5 ]; then cd $R/abtree_r5; else cd $R; fi
   timeout -k 10 300 python -u scripts/gemm_w4t_bench.py > $R/gpurun_out/r6e_w4t_$v.log 2>&1 || exit 1
