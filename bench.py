@@ -147,6 +147,8 @@ def main():
 
     # 5-minute collective timeout: a rank that fails inside the checkpoint block makes its peers
     # raise (and report the error in the JSON line) instead of blocking for the 30-minute default
+    if a.graph:
+        fdist.graph_capture_env()
     info = fdist.init_distributed(a.device, timeout_s=300)
     dev = info.device
     world = info.world_size

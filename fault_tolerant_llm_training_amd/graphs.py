@@ -110,6 +110,10 @@ class GraphedStep:
         self.opt.stage_hyper(self.opt.step_count)
         self.opt.step_count -= 1  # step() increments it again
         self._opt_step()
+        # the norm / non-finite flag were written on the optimizer (side) stream; the host copy below
+        # runs on this stream: without the join it could read the previous step's stats (a poisoned
+        # step then looked finite and was not rolled back -- a race seen once on the GPU suite)
+        self._join()
         self.opt.publish_stats()
         self.sched.step()
         self.pending = False

@@ -89,12 +89,16 @@ def set_fused_sumsq(on: bool) -> None:
     FUSED_SUMSQ = bool(on)
 
 
-def sink_partials(numel: int, ndim: int) -> int:
-    """Partial slots a sink's producers may write: one per w4 output tile (>= 256 x 128 elements)
+def sink_partials(numel: int, ndim: int, shape=None) -> int:
+    """Partial slots a sink's producers may write: one per w4 output tile (>= 256 x 128 elements,
+    a tail tile of the dW layout covering fewer: ceil(rows / 256) x ceil(cols / 128) bounds them)
     of a 2-D weight, one per 32 columns of a 1-D one; also the grid of the fallback sumsq pass."""
     if ndim <= 1:
         return max(1, (numel + 31) // 32)
-    return max(1, (numel + 32767) // 32768)
+    n = max(1, (numel + 32767) // 32768)
+    if shape is not None and len(shape) == 2:
+        n = max(n, -(-int(shape[0]) // 256) * -(-int(shape[1]) // 128))
+    return n
 
 
 def _copy_back(dst: torch.Tensor, src: torch.Tensor, temps) -> None:
@@ -226,7 +230,7 @@ class GradReducer:
             plain = [s for s in flat.sinks.values()
                      if not any(lo <= s.start and s.end <= hi for lo, hi in covered)]
             for sink in sorted(fused + plain, key=lambda s: s.start, reverse=True):
-                k = sink_partials(sink.end - sink.start, sink.buf.dim())
+                k = sink_partials(sink.end - sink.start, sink.buf.dim(), tuple(sink.buf.shape))
                 sink.part = (p, p + k)  # replaced by the tensor slice below
                 p += k
                 self._sq_sinks.append(sink)

@@ -63,6 +63,20 @@ def env_ranks():
     return 0, 1, int(env.get("LOCAL_RANK", 0))
 
 
+def graph_capture_env() -> None:
+    """Before the process group exists, for runs that capture RCCL collectives into a HIP graph.
+
+    The whole-step graph issues its collectives blocking on one stream (ddp.GradReducer
+    .single_stream). ProcessGroupNCCL hands the watchdog thread the works of those collectives,
+    captured ones included, and the watchdog's hipEventQuery on an event recorded during capture
+    fails with hipErrorCapturedEvent. By default the watchdog rethrows that and aborts the process
+    (SIGABRT, seen as a race on the 1-rank RCCL tests). With TORCH_NCCL_RETHROW_CUDA_ERRORS=0 it
+    logs the error and stops. The job loses only the watchdog's collective timeout, which this
+    framework does not rely on: a lost or hung peer is detected by the per-step gloo vote
+    (--peer-timeout) and the bounded device drain in the trainer."""
+    os.environ.setdefault("TORCH_NCCL_RETHROW_CUDA_ERRORS", "0")
+
+
 def init_distributed(device_type: str = "cuda", timeout_s: int = 1800, peer_timeout_s: float = 60.0) -> DistInfo:
     global _INFO
     if _INFO is not None:

@@ -206,6 +206,8 @@ def _build_source(args, info, tokenizer_vocab_holder: Dict[str, Any]):
 
 def train(args) -> int:
     t_setup = time.perf_counter()
+    if args.compile or args.hip_graph:
+        fdist.graph_capture_env()
     info = fdist.init_distributed(args.device, peer_timeout_s=args.peer_timeout)
     init_logger(info.rank)
     logger.info(f"Experiment args: {args}")
