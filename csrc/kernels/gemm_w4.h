@@ -213,6 +213,7 @@ struct W4Args {
   // guard skips the update and the trainer stops on it) and re-arms only the flags it saw raised
   int* err;
   int spin;              // consumer poll bound (2^22 ~ seconds; tests lower it)
+  int deadzero;          // the last two K-tiles' DMAs read nothing (null descriptor; gemm_w4_set_deadzero)
 };
 
 // (tm, tn) of workgroup bid (returned by value: through references the pair went to scratch)
@@ -308,6 +309,7 @@ struct Sched {
 
 struct Ctx {
   i32x4_t srdA, srdB;
+  i32x4_t srdA0, srdB0;             // same bases, num_records 0: every load out of range (zeros, no traffic)
   unsigned voA[8], voB[8];
   unsigned rdA0, rdA1, rdB0, rdB1;  // K-contiguous images: k-step 0 / 1 lane address
   unsigned aT[8], bT[8];            // k-major images: lane address of fragment i (k-step 0, lo)
@@ -365,8 +367,13 @@ __device__ __forceinline__ void rd_slot(Frag<AT> (&ax)[8], Frag<BT> (&bx)[NJ], c
 template <class E, int NJ, bool AT, bool BT, int CUR, bool DMA, bool NEXT>
 __device__ __forceinline__ void ktile(f32x4_t (&acc)[8][NJ], Frags<NJ, AT, BT>& f, int t, int nk, const Ctx& c) {
   using S = Sched<NJ, AT, BT>;
+  // the last two K-tiles have no tile t + 2: their DMAs go through the null descriptors (every load
+  // out of range: zeros into the dead stage, no memory request, nothing for the drain's vmcnt(0) to
+  // wait on) -- before round 6 they re-staged the last tile from L2 (W4Args::deadzero = 0)
+  const bool live = t + 2 < nk;
   const int tn2 = __builtin_amdgcn_readfirstlane(min(t + 2, nk - 1));
   const unsigned kofsA = (unsigned)tn2 * c.stepA, kofsB = (unsigned)tn2 * c.stepB;
+  const i32x4_t dsrdA = live ? c.srdA : c.srdA0, dsrdB = live ? c.srdB : c.srdB0;
   const unsigned sb = c.sbase;
   sfor<2 * S::MH>([&](auto SS) {
     constexpr int s = SS;
@@ -400,9 +407,9 @@ __device__ __forceinline__ void ktile(f32x4_t (&acc)[8][NJ], Frags<NJ, AT, BT>& 
           constexpr int qa = d < 2 * NJ ? d / 2 : NJ + (d - 2 * NJ);
           constexpr bool isA = d < 2 * NJ ? (d % 2 == 0) : true;
           if constexpr (isA)
-            dma16<S::A_AT(CUR) + qa * 4 * PIECE>(c.srdA, c.voA[qa], kofsA, sb);
+            dma16<S::A_AT(CUR) + qa * 4 * PIECE>(dsrdA, c.voA[qa], kofsA, sb);
           else
-            dma16<S::B_AT(CUR) + (d / 2) * 4 * PIECE>(c.srdB, c.voB[d / 2], kofsB, sb);
+            dma16<S::B_AT(CUR) + (d / 2) * 4 * PIECE>(dsrdB, c.voB[d / 2], kofsB, sb);
         }
       });
     }
@@ -498,6 +505,12 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(W4Args p) {
       const long src = EPI == W4_SWIGLU ? (r < 16 * NJ ? f0 + r : (long)p.ffn + f0 + (r - 16 * NJ)) : r;
       c.voB[q] = (unsigned)((src * p.ldb + lch * 8) * 2);
     }
+  }
+  c.srdA0 = c.srdA;
+  c.srdB0 = c.srdB;
+  if (p.deadzero) {
+    c.srdA0[2] = 0;
+    c.srdB0[2] = 0;
   }
   // fragment reads, K-contiguous: lane reads row r0 + (lane & 15), chunk (kk * 4 + (lane >> 4)) ^ (lane & 7)
   const unsigned lrowb = (unsigned)(((lane & 15) >> 3) * PIECE + (lane & 7) * 128);

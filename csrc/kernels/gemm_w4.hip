@@ -11,8 +11,12 @@ using namespace ftw4;
 long long* g_prof = nullptr;  // per-workgroup stamps (gemm_w4_set_prof): W4Args::prof of every launch
 long g_prof_rows = 0;         // rows of that buffer (checked against the grid at launch)
 
-void launch(at::ScalarType st_, int nj, const W4Args& p, int epi, hipStream_t st, bool at_ = false,
+extern int g_deadzero;
+
+void launch(at::ScalarType st_, int nj, const W4Args& p_, int epi, hipStream_t st, bool at_ = false,
             bool bt = false) {
+  W4Args p = p_;
+  p.deadzero = g_deadzero;
   TORCH_CHECK(p.prof == nullptr || (long)p.tiles_m * p.tiles_n * (p.splits > 1 ? p.splits : 1) <= g_prof_rows,
               "gemm_w4_set_prof: the buffer needs one row of 8 int64 per workgroup");
   // the step's layouts: forward (K-contiguous both), dX (k-major B), dW (k-major both)
@@ -147,6 +151,12 @@ int* splitk_ticks(const c10::Device& dev, hipStream_t st, long n) {
 // stream). Falls back to one workgroup per tile where the split cannot run.
 int g_dbg = 0;  // timing probes (gemm_w4_set_dbg): W4Args::dbg of every launch
 int g_spin = 1 << 22;  // split-K consumer poll bound (gemm_w4_set_spin: tests of the timeout path)
+// The last two K-tiles' DMAs (no tile t + 2 to fetch) through null descriptors instead of
+// re-staging the last tile (gemm_w4_set_deadzero, FT_W4_DEADZERO: A/B)
+int g_deadzero = [] {
+  const char* e = std::getenv("FT_W4_DEADZERO");
+  return e == nullptr ? 1 : std::atoi(e);
+}();
 // Grouped tile raster (W4Args::group, tile_of): the XCD's 32 concurrent tiles as a G x 32/G block.
 // -1 (default): 8 for the dW layout (k-major A), 4 or 8 per entry otherwise; >= 0 forces (0: plain).
 // Measured per 8B product (scripts/w4_raster_bench.py, profiles/r5_w4_raster_sweep2.log): w13 dW
@@ -492,6 +502,7 @@ int64_t gemm_w4_splitk_errors(bool reset) {
 
 // split-K consumer poll bound (tests of the timeout path; default 2^22)
 void gemm_w4_set_spin(int64_t n) { g_spin = (int)std::max<int64_t>(1, n); }
+void gemm_w4_set_deadzero(int64_t on) { g_deadzero = (int)on; }
 
 // timing probes only (scripts/w4_overhead_probe.py): bit 0 skips the store / residual epilogues'
 // global stores (the output is left unwritten)
@@ -526,6 +537,7 @@ TORCH_LIBRARY_FRAGMENT(ftamd, m) {
   m.def("gemm_w4_prepare_capture() -> ()", &gemm_w4_prepare_capture);
   m.def("gemm_w4_splitk_errors(bool reset=False) -> int", &gemm_w4_splitk_errors);
   m.def("gemm_w4_set_spin(int n) -> ()", &gemm_w4_set_spin);
+  m.def("gemm_w4_set_deadzero(int on) -> ()", &gemm_w4_set_deadzero);
   m.def("gemm_w4_set_dbg(int v) -> ()", &gemm_w4_set_dbg);
   m.def("gemm_w4_set_group(int v) -> ()", &gemm_w4_set_group);
   m.def("gemm_w4_set_prof(Tensor? buf) -> ()", &gemm_w4_set_prof);

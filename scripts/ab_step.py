@@ -26,6 +26,8 @@ Knobs toggled between timing windows (alternating rounds, so box and clock drift
   r4    — w4bwd + psums + w4head together (round-4 routing vs round-3)
   deepdx — the deep-reduction dX products (8B w13 dX, LM-head dX) on hipBLASLt instead of the w4 kernel
   w4dwside — the w4 weight gradients on the dW side stream (default: inline on the compute stream)
+  deadzero — the w4 GEMM's last two K-tiles issue their (dead) LDS-DMAs through null descriptors
+          instead of re-staging the last K-tile (round 6)
 Usage: python scripts/ab_step.py [--steps 8] [--rounds 3] [--configs gemm,dw ...]
 """
 from __future__ import annotations
@@ -117,7 +119,8 @@ def main():
                "w4dwside": lambda on: (torch.cuda.synchronize(), setattr(Fx, "_W4_DW_SIDE", on)),
                "gemm_s": lambda on: (torch.cuda.synchronize(), Fx.set_gemm_s(on)),
                "adamw_serial": lambda on: serial_adamw.__setitem__(0, bool(on)),
-               "raster": lambda on: (torch.cuda.synchronize(), kernels().gemm_w4_set_group(-1 if on else 0))}
+               "raster": lambda on: (torch.cuda.synchronize(), kernels().gemm_w4_set_group(-1 if on else 0)),
+               "deadzero": lambda on: (torch.cuda.synchronize(), kernels().gemm_w4_set_deadzero(1 if on else 0))}
     configs = list(itertools.product([False, True], repeat=len(knobs)))
 
     def apply(cfg):
