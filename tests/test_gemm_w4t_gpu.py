@@ -342,3 +342,30 @@ def test_w4_grouped_raster_bitwise(group):
     for r_, g_ in zip(ref, got):
         for u, v in zip(r_, g_):
             assert torch.equal(u, v)
+
+
+def test_dead_tail_dmas_change_nothing():
+    """gemm_w4_set_deadzero (FT_W4_DEADZERO): the last two K-tiles' LDS-DMAs (no tile t + 2 to fetch)
+    through null descriptors (zeros into the dead stage, no memory traffic) or re-staging the last
+    K-tile: bitwise the same products in every layout, split-K and epilogue."""
+    k = K()
+    torch.manual_seed(21)
+    a, b = rnd(1024, 1024), rnd(768, 1024)
+    a2, b2 = rnd(512, 4096), rnd(4096, 1024)
+    at, x = rnd(2048, 2304), rnd(2048, 768)
+    part = torch.zeros(64, device="cuda")
+    cases = [lambda: k.gemm_nt_w4(a, b, None, None, 0, 0),
+             lambda: k.gemm_w4_ex(a2, False, b2, True, 512, 1024, 4096, None, False, None, 8, 2),
+             lambda: (k.gemm_w4_ex(at, True, x, True, 2304, 768, 2048, None, False, part, 4, 3), part.clone()),
+             lambda: k.gemm_swiglu_w4(a, rnd(2 * 448, 1024), False)[:2]]
+    torch.manual_seed(22)
+    ref = [f() for f in cases]
+    try:
+        k.gemm_w4_set_deadzero(0)
+        torch.manual_seed(22)
+        got = [f() for f in cases]
+    finally:
+        k.gemm_w4_set_deadzero(1)
+    for r_, g_ in zip(ref, got):
+        for u, v in zip(r_ if isinstance(r_, tuple) else (r_,), g_ if isinstance(g_, tuple) else (g_,)):
+            assert torch.equal(u, v)

@@ -92,3 +92,15 @@ def test_fp32_model_logs_the_hipblaslt_fallback_once(tmp_path):
     rc, out = run_train(d, "4102", TINY + ["--synthetic-data", "--vocab-size", "256", "--training-steps", "2",
                                            "--checkpoint-path", os.path.join(d, "ck")])
     assert rc == 0 and "GEMMs on hipBLASLt" not in out
+
+
+def test_qkv_rope_min_k_knob(monkeypatch):
+    """FT_QKV_ROPE_MIN_K (ops/attention.py): the QKV projection with the RoPE epilogue from this model
+    dim; 2048 by default (the 8B class), so GPT-2 (768 / 1024) keeps the separate RoPE kernel (the
+    fused form measured 0.6-0.7 % slower there: profiles/r6/gpt2_graph_ab.log)."""
+    from fault_tolerant_llm_training_amd.ops import attention as A
+
+    a = model_args_for("gpt2-small", vocab_size=50304, seq_len=2048)
+    assert routing_table(a, torch.bfloat16)["qkv fwd"] == "w4 128"
+    monkeypatch.setattr(A, "_QKV_ROPE_MIN_K", 768)
+    assert routing_table(a, torch.bfloat16)["qkv fwd"] == "w4 qkv+rope"
