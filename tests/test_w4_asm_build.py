@@ -64,8 +64,11 @@ def test_reintroduced_scc_clobber_fails_the_check(tmp_path):
     hdr = (KDIR / "gemm_w4.h").read_text()
     assert hdr.count(': "memory", "scc");') == 1  # the LDS-DMA asm declares its SCC write
     (tmp_path / "gemm_w4.h").write_text(hdr.replace(': "memory", "scc");', ': "memory");'))
-    shutil.copy(KDIR / "gemm_w4_fwd.hip", tmp_path / "gemm_w4_fwd.hip")
-    asm = _compile_s(tmp_path / "gemm_w4_fwd.hip", tmp_path / "fwd.s", include_first=tmp_path)
+    # the dX translation unit: since round 6 the forward one keeps its K-loop condition out of SCC
+    # (the dead-tail descriptor selects read SCC right after their compare), so the undeclared
+    # clobber has nothing to corrupt there; the dX / dW loops still branch on SCC
+    shutil.copy(KDIR / "gemm_w4_dx.hip", tmp_path / "gemm_w4_dx.hip")
+    asm = _compile_s(tmp_path / "gemm_w4_dx.hip", tmp_path / "dx.s", include_first=tmp_path)
     n, bad = _w4check.check_asm(asm)
     assert n > 0 and bad, "the SCC clobber was not detected"
     assert any("between" in e for _, errs in bad for e in errs)
