@@ -153,6 +153,11 @@ int g_dbg = 0;  // timing probes (gemm_w4_set_dbg): W4Args::dbg of every launch
 int g_spin = 1 << 22;  // split-K consumer poll bound (gemm_w4_set_spin: tests of the timeout path)
 // The last two K-tiles' DMAs (no tile t + 2 to fetch) through null descriptors instead of
 // re-staging the last tile (gemm_w4_set_deadzero, FT_W4_DEADZERO: A/B)
+// Round-remainder split of a 1.5-round dW grid (gemm_w4_ex; gemm_w4_set_remainder, FT_W4_REMAINDER: A/B)
+int g_remainder = [] {
+  const char* e = std::getenv("FT_W4_REMAINDER");
+  return e == nullptr ? 1 : std::atoi(e);
+}();
 int g_deadzero = [] {
   const char* e = std::getenv("FT_W4_DEADZERO");
   return e == nullptr ? 1 : std::atoi(e);
@@ -282,36 +287,62 @@ at::Tensor gemm_w4_ex(const at::Tensor& a, bool a_t, const at::Tensor& b, bool b
     TORCH_CHECK(!accumulate, "gemm_w4_ex: accumulate needs out");
     c = at::empty({M, N}, a.options());
   }
-  W4Args p{};
-  p.prof = g_prof;
-  p.group = raster_group(false);
-  p.a = cptr<bf16_t>(a);
-  p.b = cptr<bf16_t>(b);
-  p.c = mptr<bf16_t>(c);
-  p.r = accumulate ? cptr<bf16_t>(c) : nullptr;
-  p.lda = a_t ? M : K;
-  p.ldb = b_t ? N : K;
-  p.ldc = N;
-  p.ldr = N;
-  p.M = M;
-  p.N = N;
-  p.K = K;
-  p.tiles_m = (M + BM - 1) / BM;
-  p.tiles_n = N / (32 * NJ);
-  p.nfast = M > N;  // keep the larger operand's panels inside one XCD
-  p.group = raster_group(a_t);
+  float* part_p = nullptr;
+  int part_n = 0;
   if (part.has_value() && part->defined()) {
     FT_CHECK_F32((*part));
     FT_CHECK_CONTIG((*part));
-    TORCH_CHECK(part->numel() >= (long)p.tiles_m * p.tiles_n, "gemm_w4_ex: part holds ", part->numel(),
-                " partials, need ", (long)p.tiles_m * p.tiles_n);
-    p.part = mptr<float>(*part);
-    p.part_n = (int)part->numel();
+    const long need = ((M + BM - 1) / BM) * (N / (32 * NJ));
+    TORCH_CHECK(part->numel() >= need, "gemm_w4_ex: part holds ", part->numel(), " partials, need ", need);
+    part_p = mptr<float>(*part);
+    part_n = (int)part->numel();
   }
-  at::Tensor ws;
-  setup_split(p, pl.splits, NJ, a, ws, a_t);
-  launch(a.scalar_type(), NJ, p, accumulate ? W4_RES : W4_STORE, ft_stream(), a_t, b_t);
-  FT_LAUNCH_CHECK();
+  // rows [m_off, m_off + Ms) at tile width nj_: C rows and (k-major A) A columns offset, partials
+  // from part_p + p_off (part[tn * tiles_m + tm] of this launch's grid)
+  auto run = [&](long m_off, long Ms, int nj_, int splits_, long p_off) {
+    W4Args p{};
+    p.prof = g_prof;
+    p.a = cptr<bf16_t>(a) + (a_t ? m_off : m_off * K);
+    p.b = cptr<bf16_t>(b);
+    p.c = mptr<bf16_t>(c) + m_off * N;
+    p.r = accumulate ? p.c : nullptr;
+    p.lda = a_t ? M : K;
+    p.ldb = b_t ? N : K;
+    p.ldc = N;
+    p.ldr = N;
+    p.M = Ms;
+    p.N = N;
+    p.K = K;
+    p.tiles_m = (Ms + BM - 1) / BM;
+    p.tiles_n = N / (32 * nj_);
+    p.nfast = Ms > N;  // keep the larger operand's panels inside one XCD
+    p.group = raster_group(a_t);
+    if (part_p != nullptr) {
+      p.part = part_p + p_off;
+      p.part_n = part_n - (int)p_off;
+    }
+    at::Tensor ws;
+    setup_split(p, splits_, nj_, a, ws, a_t);
+    launch(a.scalar_type(), nj_, p, accumulate ? W4_RES : W4_STORE, ft_stream(), a_t, b_t);
+    FT_LAUNCH_CHECK();
+  };
+  // Round remainder (automatic plan, dW layout): one full round of 256-wide tiles plus at most half
+  // a round (the 8B qkv dW: 24 x 16 tiles = 1.5 rounds, its last round half idle) runs as two
+  // launches over disjoint rows -- the full round at 256 columns, the remaining row tiles at the
+  // 128-wide tile (twice as many tiles of half the work: one more full round). Same per-element
+  // summation order, so bitwise the single launch's result (gemm_w4_set_remainder: A/B).
+  if (nj <= 0 && a_t && g_remainder && pl.splits == 1 && NJ == 8 && N % 128 == 0 && M % BM == 0) {
+    const long tn = N / 256, tm = M / BM;
+    if (256 % tn == 0) {
+      const long full = 256 / tn;  // row tiles of one round
+      if (tm > full && (tm - full) * tn * 2 <= 256) {
+        run(0, full * BM, 8, 1, 0);
+        run(full * BM, M - full * BM, 4, 1, 256);
+        return c;
+      }
+    }
+  }
+  run(0, M, NJ, pl.splits, 0);
   return c;
 }
 
@@ -503,6 +534,7 @@ int64_t gemm_w4_splitk_errors(bool reset) {
 // split-K consumer poll bound (tests of the timeout path; default 2^22)
 void gemm_w4_set_spin(int64_t n) { g_spin = (int)std::max<int64_t>(1, n); }
 void gemm_w4_set_deadzero(int64_t on) { g_deadzero = (int)on; }
+void gemm_w4_set_remainder(int64_t on) { g_remainder = (int)on; }
 
 // timing probes only (scripts/w4_overhead_probe.py): bit 0 skips the store / residual epilogues'
 // global stores (the output is left unwritten)
@@ -538,6 +570,7 @@ TORCH_LIBRARY_FRAGMENT(ftamd, m) {
   m.def("gemm_w4_splitk_errors(bool reset=False) -> int", &gemm_w4_splitk_errors);
   m.def("gemm_w4_set_spin(int n) -> ()", &gemm_w4_set_spin);
   m.def("gemm_w4_set_deadzero(int on) -> ()", &gemm_w4_set_deadzero);
+  m.def("gemm_w4_set_remainder(int on) -> ()", &gemm_w4_set_remainder);
   m.def("gemm_w4_set_dbg(int v) -> ()", &gemm_w4_set_dbg);
   m.def("gemm_w4_set_group(int v) -> ()", &gemm_w4_set_group);
   m.def("gemm_w4_set_prof(Tensor? buf) -> ()", &gemm_w4_set_prof);

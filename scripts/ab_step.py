@@ -28,6 +28,8 @@ Knobs toggled between timing windows (alternating rounds, so box and clock drift
   w4dwside — the w4 weight gradients on the dW side stream (default: inline on the compute stream)
   deadzero — the w4 GEMM's last two K-tiles issue their (dead) LDS-DMAs through null descriptors
           instead of re-staging the last K-tile (round 6)
+  remainder — a 1.5-round dW grid (the 8B qkv dW) as a full round of 256-wide tiles plus the
+          remaining rows at the 128-wide tile (round 6)
 Usage: python scripts/ab_step.py [--steps 8] [--rounds 3] [--configs gemm,dw ...]
 """
 from __future__ import annotations
@@ -120,7 +122,8 @@ def main():
                "gemm_s": lambda on: (torch.cuda.synchronize(), Fx.set_gemm_s(on)),
                "adamw_serial": lambda on: serial_adamw.__setitem__(0, bool(on)),
                "raster": lambda on: (torch.cuda.synchronize(), kernels().gemm_w4_set_group(-1 if on else 0)),
-               "deadzero": lambda on: (torch.cuda.synchronize(), kernels().gemm_w4_set_deadzero(1 if on else 0))}
+               "deadzero": lambda on: (torch.cuda.synchronize(), kernels().gemm_w4_set_deadzero(1 if on else 0)),
+               "remainder": lambda on: (torch.cuda.synchronize(), kernels().gemm_w4_set_remainder(1 if on else 0))}
     configs = list(itertools.product([False, True], repeat=len(knobs)))
 
     def apply(cfg):

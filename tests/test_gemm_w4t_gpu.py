@@ -369,3 +369,33 @@ def test_dead_tail_dmas_change_nothing():
     for r_, g_ in zip(ref, got):
         for u, v in zip(r_ if isinstance(r_, tuple) else (r_,), g_ if isinstance(g_, tuple) else (g_,)):
             assert torch.equal(u, v)
+
+
+def test_round_remainder_split_bitwise():
+    """gemm_w4_set_remainder (FT_W4_REMAINDER): a dW grid of one full round plus half a round (the 8B
+    qkv dW, 24 x 16 tiles of 256^2) runs as two launches over disjoint rows, the remainder at the
+    128-wide tile. Same summation order per element: bitwise the single launch; the partial sums of
+    squares cover the same values; accumulate too."""
+    k = K()
+    torch.manual_seed(31)
+    M, N, T = 6144, 4096, 2048
+    at, x = rnd(T, M), rnd(T, N)
+    part = torch.zeros(768, device="cuda")
+
+    def go():
+        part.fill_(5.0)
+        c = k.gemm_w4_ex(at, True, x, True, M, N, T, None, False, part, 0, 0)
+        c2 = c.clone()
+        k.gemm_w4_ex(at, True, x, True, M, N, T, c2, True, None, 0, 0)
+        return c, c2, part.double().sum().item(), part[512:].abs().sum().item()
+
+    c_on, acc_on, sq_on, rest_on = go()
+    try:
+        k.gemm_w4_set_remainder(0)
+        c_off, acc_off, sq_off, rest_off = go()
+    finally:
+        k.gemm_w4_set_remainder(1)
+    assert torch.equal(c_on, c_off) and torch.equal(acc_on, acc_off)
+    assert rest_on == 0 and abs(sq_on - sq_off) <= 1e-5 * sq_off
+    want = c_on.float().pow(2).sum().item()
+    assert abs(sq_on - want) <= 1e-5 * want
