@@ -226,7 +226,9 @@ __global__ __launch_bounds__(NT, 2) void gemm_s_kernel(SArgs p) {
       }
   }
 
-  // ---- epilogue through LDS: tile rows of 256 B, chunk c at c ^ (row & 15)
+  // ---- epilogue through LDS: tile rows of 256 B, chunk c at c ^ (row & 15), its 8-B halves
+  // exchanged in rows with bit 3 set: a 16-lane ds_write_b64 group (rows lr = 0..15) then covers
+  // all 32 write banks ((a / 4) % 32) instead of 16 (as gemm_w4.h's epilogue)
   __syncthreads();  // every wave's last fragment reads are done (no DMA is in flight)
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -238,7 +240,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_s_kernel(SArgs p) {
       uint2 o;
       o.x = pk2<E>(v[0], v[1]);
       o.y = pk2<E>(v[2], v[3]);
-      *reinterpret_cast<uint2*>(smem + row * 256 + ((ch ^ (row & 15)) << 4) + (hc & 1) * 8) = o;
+      *reinterpret_cast<uint2*>(smem + row * 256 + ((ch ^ (row & 15)) << 4) + (((hc ^ (row >> 3)) & 1) << 3)) = o;
     }
   }
   __syncthreads();
@@ -247,6 +249,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_s_kernel(SArgs p) {
   for (int rr = 0; rr < 8; ++rr) {
     const int row = rr * 16 + (tid >> 4);
     uint4 v = *reinterpret_cast<const uint4*>(smem + row * 256 + ((cc ^ (row & 15)) << 4));
+    if (row & 8) v = make_uint4(v.z, v.w, v.x, v.y);
     const long gm = m0 + row;
     const int gn = n0 + cc * 8;
     if constexpr (RES) {

@@ -132,6 +132,11 @@ __device__ __forceinline__ void vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
 }
 __device__ __forceinline__ void barrier() { asm volatile("s_barrier" ::: "memory"); }
+// an epilogue staging chunk with its 8-B halves exchanged when s (rows with bit 3 set; see the
+// epilogue): the same call converts either way
+__device__ __forceinline__ uint4 stg_swap(uint4 v, bool s) {
+  return s ? make_uint4(v.z, v.w, v.x, v.y) : v;
+}
 
 // ---- fragments: one 128-bit register (ds_read_b128) or two 64-bit halves (two tr reads) ------
 template <bool T>
@@ -685,7 +690,12 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(W4Args p) {
     }
   }
 
-  // ---- epilogue through LDS: quadrant rows of 256 B (NW * 2 used), chunk c at c ^ (row & 15)
+  // ---- epilogue through LDS: quadrant rows of 256 B (NW * 2 used), chunk c at c ^ (row & 15),
+  // its two 8-B halves swapped in rows with bit 3 set (stg_swap): a fragment write is a
+  // ds_write_b64 whose 16-lane groups hold rows lr = 0..15 of one column chunk; banks are
+  // (a / 4) % 32 for every LDS write, so the XOR alone puts them on 8 chunk positions x 1 half
+  // = 16 of the 32 banks (2-way, 4 extra cycles per write: the 1024 SQ_LDS_BANK_CONFLICT per
+  // tile of round 5); the half swap gives 8 x 2 = all 32
   barrier();  // every wave is done with the stages before they become epilogue staging
   char* wl = smem + wid * 32768;
   {
@@ -726,7 +736,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(W4Args p) {
         uint2 pk;
         pk.x = pk2<E>(v[0], v[1]);
         pk.y = pk2<E>(v[2], v[3]);
-        *reinterpret_cast<uint2*>(wl + m * 256 + ((ch ^ (m & 15)) << 4) + (hc & 1) * 8) = pk;
+        *reinterpret_cast<uint2*>(wl + m * 256 + ((ch ^ (m & 15)) << 4) + (((hc ^ (m >> 3)) & 1) << 3)) = pk;
       }
     }
   }
@@ -756,7 +766,8 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(W4Args p) {
         for (int q = 0; q < 16; ++q) {
           const int row = (hb * 16 + q) * 4 + (lane >> 4);
           const long gm = m0 + wm * 128 + row;
-          const uint4 v = *reinterpret_cast<const uint4*>(wl + row * 256 + ((cc ^ (row & 15)) << 4));
+          const uint4 v = stg_swap(*reinterpret_cast<const uint4*>(wl + row * 256 + ((cc ^ (row & 15)) << 4)),
+                                   (q >> 1) & 1);  // (row & 8: constant in the unrolled loop)
           // v = da (bf16, as the unfused path's GEMM output) for features gn .. gn + 7 of token gm:
           // dg, du from the saved g = gu[gm, gn], u = gu[gm, F + gn] (swiglu_grad, common.h)
           float d8[8], g8[8], u8[8], dg[8], du[8];
@@ -775,14 +786,17 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(W4Args p) {
     // other tile runs without the per-row compare (mtail is uniform; only the dW layout has tails)
     auto store_rows = [&](auto tail_tag) {
       constexpr bool TAIL = decltype(tail_tag)::value;
-#pragma unroll 4
-      for (int rr = 0; rr < 32; ++rr) {
+      for (int r4 = 0; r4 < 32; r4 += 4)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int rr = r4 + u;
         const int row = rr * 4 + (lane >> 4);
         const long gm = m0 + wm * 128 + row;
         if constexpr (TAIL) {
           if (gm >= p.M) continue;
         }
-        uint4 v = *reinterpret_cast<const uint4*>(wl + row * 256 + ((cc ^ (row & 15)) << 4));
+        uint4 v = stg_swap(*reinterpret_cast<const uint4*>(wl + row * 256 + ((cc ^ (row & 15)) << 4)),
+                           u >> 1);  // row & 8 == (rr & 2) * 4: constant per unrolled copy
         // W4_SWIGLU: wave column half 0 holds g (gu columns [0, F)), half 1 holds u ([F, 2F))
         const int gn = EPI == W4_SWIGLU ? (wn ? p.ffn : 0) + f0 + cc * 8 : n0 + wn * NW + cc * 8;
         if constexpr (EPI == W4_RES) {
@@ -848,18 +862,20 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(W4Args p) {
     char* gl = smem + (wm * 2) * 32768;      // g quadrant of this row half
     char* ul = smem + (wm * 2 + 1) * 32768;  // u quadrant
     if (cc < 2 * NJ) {
-#pragma unroll 4
-      for (int rr = 0; rr < 16; ++rr) {
-        const int row = wn * 64 + rr * 4 + (lane >> 4);
+      for (int r4 = 0; r4 < 16; r4 += 4)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int row = wn * 64 + (r4 + u) * 4 + (lane >> 4);
         const int off = row * 256 + ((cc ^ (row & 15)) << 4);
+        const bool sw = u >> 1;  // row & 8
         float g8[8], u8[8], a8[8];
-        unpack8e<E>(*reinterpret_cast<const uint4*>(gl + off), g8);
-        unpack8e<E>(*reinterpret_cast<const uint4*>(ul + off), u8);
+        unpack8e<E>(stg_swap(*reinterpret_cast<const uint4*>(gl + off), sw), g8);
+        unpack8e<E>(stg_swap(*reinterpret_cast<const uint4*>(ul + off), sw), u8);
 #pragma unroll
         for (int q = 0; q < 8; ++q) a8[q] = g8[q] * sigmoid_f(g8[q], p.exact) * u8[q];
         const uint4 av = pack8e<E>(a8);
         *reinterpret_cast<uint4*>(p.act + (m0 + wm * 128 + row) * (long)p.ffn + f0 + cc * 8) = av;
-        *reinterpret_cast<uint4*>(gl + off) = av;
+        *reinterpret_cast<uint4*>(gl + off) = stg_swap(av, sw);
       }
     }
     if (p.actT == nullptr) {  // uniform
@@ -878,7 +894,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_w4_kernel(W4Args p) {
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         const int row = tg * 8 + i;
-        const uint4 v = *reinterpret_cast<const uint4*>(al + row * 256 + ((fc ^ (row & 15)) << 4));
+        const uint4 v = stg_swap(*reinterpret_cast<const uint4*>(al + row * 256 + ((fc ^ (row & 15)) << 4)), tg & 1);
         const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
