@@ -1,0 +1,403 @@
+// fp32 GEMM on the CDNA4 matrix cores (v_mfma_f32_16x16x4_f32) for --model-dtype fp32: the forward,
+// dX and dW products of every nn.Linear (reference model.py:195,215,254,379, utils.py:14-19), which
+// the 16-bit w4 / s kernels do not take.
+//
+//   C[M, N] (+)= sum_k A(m, k) * B(n, k) (+ residual)
+//   A(m, k) = a[m * lda + k] (a_t = false) or a[k * lda + m] (a_t = true)
+//   B(n, k) = b[n * ldb + k] (b_t = false) or b[k * ldb + n] (b_t = true)
+//   forward x W^T: (false, false); dX = dY W: (false, true); dW = dY^T X: (true, true) -- the same
+//   layout flags as gemm_w4_ex, so ops/functional.py routes the three products the same way.
+//
+// Why a different shape from the 16-bit kernels: fp32 MFMA is 1/16 of the bf16 rate per byte of
+// operand (16x16x4 = 2 kFLOP per 32-cycle issue from 512 B of operands vs 16x16x32 bf16 = 16 kFLOP
+// per 8 cycles from 2 KiB), so the kernel is MFMA-bound with plain LDS traffic and no split-K:
+//   * 128 x 128 tile, BK = 32, 4 waves (2 x 2), each a 64 x 64 quadrant = 4 x 4 accumulators of
+//     16 x 16; two workgroups per CU (80 KiB of LDS each), so one's barrier / epilogue runs while
+//     the other issues MFMAs.
+//   * Operands global -> registers (float4, the next K-tile in flight during the current one's
+//     MFMAs) -> LDS in the layout they have in HBM: k-contiguous operands as [row][40] (32 k + 8
+//     pad: the ds_read_b128 fragment reads are conflict-free), row-contiguous (k-major) ones as
+//     [k][132] (lanes 16-31 read 4 k-rows further = 16 banks away). One barrier per K-tile
+//     (double-buffered LDS).
+//   * K order inside a 16-deep chunk: MFMA j of the chunk takes k = 4 g + j from lane group
+//     g = lane / 16, so a lane's four MFMAs read one float4 of its row (k-contiguous images).
+//   * Grids of less than one tile per CU (the GPT-2-sized products: 96 tiles at T = 2048) split K
+//     into S slices: each writes its raw fp32 partial to a workspace and a reduction pass sums the
+//     slices in order 0 .. S-1 (deterministic) and applies the epilogue.
+//   * Epilogue from the accumulators: 16 lanes store 64 contiguous bytes of a row; optional
+//     accumulate (gradient accumulation), + residual (fused residual add), and one sum-of-squares
+//     partial per tile for the global gradient norm (as the w4 dW epilogue: part[tn * tiles_m + tm]).
+//   * Tiles XCD-contiguous (workgroup t on XCD t % 8 takes a contiguous M-fastest range), so an
+//     operand panel is shared through one L2.
+#include "torch_utils.h"
+
+namespace {
+
+constexpr int BM = 128, BN = 128, BK = 32, NT = 256;
+constexpr int SK = BK + 8;    // floats per row of a k-contiguous image
+constexpr int SR = BM + 4;    // floats per k-row of a row-contiguous image
+constexpr int IMG = BM * SK;  // floats per operand image (5120 >= BK * SR = 4224)
+static_assert(BK * SR <= IMG, "image size");
+constexpr int LDS_FLOATS = 2 * 2 * IMG;  // 2 stages x (A, B): 80 KiB
+
+struct F32Args {
+  const float* a;
+  const float* b;
+  float* c;
+  const float* r;  // residual [M, N] or null
+  float* part;     // per-tile sums of squares or null
+  long lda, ldb, ldc, ldr;
+  int M, N, K;
+  int tiles_m, tiles_n, part_n;
+  int acc;  // C += instead of C =
+  int ks;     // K slices (1: none)
+  float* ws;  // ks > 1: raw partials [ks][M][N]
+};
+
+__device__ __forceinline__ void tile_of(int t, int tiles_m, int tiles_n, int& tm, int& tn) {
+  const int nwg = tiles_m * tiles_n;
+  const int q = nwg / 8, rem = nwg % 8;
+  const int x = t % 8, o = t / 8;
+  const int w = (x < rem ? x * (q + 1) : rem * (q + 1) + (x - rem) * q) + o;
+  tm = w % tiles_m;
+  tn = w / tiles_m;
+}
+
+// One operand's K-tile: global -> 4 float4 registers per thread. RC (row-contiguous, k-major):
+// 32 k-rows x 32 float4; otherwise 128 rows x 8 float4. Rows past `rows` are clamped (their
+// products land in C rows / columns that are never stored) or, row-contiguous, zero-filled
+// (rows % 4 == 0, checked on the host, keeps a float4 inside or outside).
+template <bool RC>
+__device__ __forceinline__ void load_tile(const float* __restrict__ x, long ld, int i0, int rows, int k0, int tid,
+                                          float4 (&v)[4]) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int idx = q * NT + tid;
+    if constexpr (RC) {
+      const int k = idx >> 5, c4 = idx & 31;
+      const int i = i0 + 4 * c4;
+      v[q] = i < rows ? *reinterpret_cast<const float4*>(x + (long)(k0 + k) * ld + i) : make_float4(0.f, 0.f, 0.f, 0.f);
+    } else {
+      const int row = idx >> 3, c4 = idx & 7;
+      const int i = min(i0 + row, rows - 1);
+      v[q] = *reinterpret_cast<const float4*>(x + (long)i * ld + k0 + 4 * c4);
+    }
+  }
+}
+
+template <bool RC>
+__device__ __forceinline__ void store_tile(float* img, int tid, const float4 (&v)[4]) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int idx = q * NT + tid;
+    if constexpr (RC)
+      *reinterpret_cast<float4*>(img + (idx >> 5) * SR + 4 * (idx & 31)) = v[q];
+    else
+      *reinterpret_cast<float4*>(img + (idx >> 3) * SK + 4 * (idx & 7)) = v[q];
+  }
+}
+
+// f[j] = X(row base + lane % 16, k = 16 c + 4 (lane / 16) + j) from an image
+template <bool RC>
+__device__ __forceinline__ float4 frag(const float* img, int base, int c, int lane) {
+  const int r16 = lane & 15, g = lane >> 4;
+  if constexpr (RC) {
+    const float* p = img + (16 * c + 4 * g) * SR + base + r16;
+    return make_float4(p[0], p[SR], p[2 * SR], p[3 * SR]);
+  } else {
+    return *reinterpret_cast<const float4*>(img + (base + r16) * SK + 16 * c + 4 * g);
+  }
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <bool AT, bool BT, bool RES, bool PART>
+__global__ __launch_bounds__(NT, 2) void gemm_f32_kernel(F32Args p) {
+  __shared__ __attribute__((aligned(16))) float smem[LDS_FLOATS];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 1, wn = wid & 1;
+  const int ntile = p.tiles_m * p.tiles_n;
+  const int slice = blockIdx.x / ntile;
+  int tm, tn;
+  tile_of(blockIdx.x - slice * ntile, p.tiles_m, p.tiles_n, tm, tn);
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int nk_all = p.K / BK, per = (nk_all + p.ks - 1) / p.ks;
+  const int kb = slice * per * BK;  // this slice's first k
+  const int nk = min(per, nk_all - slice * per);
+
+  f32x4_t acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  float4 ra[4], rb[4];
+  load_tile<AT>(p.a, p.lda, m0, p.M, kb, tid, ra);
+  load_tile<BT>(p.b, p.ldb, n0, p.N, kb, tid, rb);
+  store_tile<AT>(smem, tid, ra);
+  store_tile<BT>(smem + IMG, tid, rb);
+  __syncthreads();
+
+  // fragment registers of the two 16-deep chunks of a K-tile: chunk 1 is read before the barrier
+  // and multiplied after it, under the next K-tile's chunk-0 reads (the LDS latency and the
+  // barrier's skew hide under 64 MFMAs instead of stalling every wave at the top of the tile)
+  float4 fa[2][4], fb[2][4];
+  auto read = [&](const float* ia, int c, float4 (&xa)[4], float4 (&xb)[4]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) xa[i] = frag<AT>(ia, wm * 64 + i * 16, c, lane);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) xb[j] = frag<BT>(ia + IMG, wn * 64 + j * 16, c, lane);
+  };
+  auto mma = [&](const float4 (&xa)[4], const float4 (&xb)[4]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float av = q == 0 ? xa[i].x : q == 1 ? xa[i].y : q == 2 ? xa[i].z : xa[i].w;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float bv = q == 0 ? xb[j].x : q == 1 ? xb[j].y : q == 2 ? xb[j].z : xb[j].w;
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[i][j], 0, 0, 0);
+        }
+      }
+    }
+  };
+  static_assert(BK == 32, "two 16-deep chunks per K-tile");
+  read(smem, 0, fa[0], fb[0]);
+  for (int kt = 0; kt < nk; ++kt) {
+    const float* cur = smem + (kt & 1) * 2 * IMG;
+    float* nxt = smem + ((kt + 1) & 1) * 2 * IMG;
+    // the next K-tile's loads in flight under this one's MFMAs; unconditional (the last iteration
+    // reloads its own tile into the idle buffer): with the loads and stores under a branch the
+    // compiler parked the prefetch registers in scratch memory, waiting on each load at once
+    const int kn = kb + min(kt + 1, nk - 1) * BK;
+    load_tile<AT>(p.a, p.lda, m0, p.M, kn, tid, ra);
+    load_tile<BT>(p.b, p.ldb, n0, p.N, kn, tid, rb);
+    read(cur, 1, fa[1], fb[1]);
+    mma(fa[0], fb[0]);
+    store_tile<AT>(nxt, tid, ra);
+    store_tile<BT>(nxt + IMG, tid, rb);
+    __syncthreads();
+    read(nxt, 0, fa[0], fb[0]);  // (after the last K-tile: a harmless read of the idle buffer)
+    mma(fa[1], fb[1]);
+  }
+  __syncthreads();  // every wave's last (idle-buffer) reads are done before smem is reused
+
+  // epilogue: acc[i][j][v] = C(m0 + 64 wm + 16 i + 4 (lane / 16) + v, n0 + 64 wn + 16 j + lane % 16)
+  const int g = lane >> 4, r16 = lane & 15;
+  if (p.ks > 1) {  // a slice's raw partial (f32_splitk_reduce applies the epilogue)
+    float* w = p.ws + (long)slice * p.M * p.N;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int m = m0 + wm * 64 + i * 16 + 4 * g + v;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int n = n0 + wn * 64 + j * 16 + r16;
+          if (m < p.M && n < p.N) w[(long)m * p.N + n] = acc[i][j][v];
+        }
+      }
+    return;
+  }
+  float sq = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int m = m0 + wm * 64 + i * 16 + 4 * g + v;
+      if (m >= p.M) continue;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = n0 + wn * 64 + j * 16 + r16;
+        if (n >= p.N) continue;
+        float* cp = p.c + (long)m * p.ldc + n;
+        float x = acc[i][j][v];
+        if (p.acc) x += *cp;
+        if constexpr (RES) x += p.r[(long)m * p.ldr + n];
+        if constexpr (PART) sq = fmaf(x, x, sq);
+        *cp = x;
+      }
+    }
+  if constexpr (PART) {  // one partial per tile, fixed order (deterministic)
+    sq = wave_sum(sq);
+    if (lane == 0) smem[wid] = sq;
+    __syncthreads();
+    if (tid == 0) p.part[tn * p.tiles_m + tm] = (smem[0] + smem[1]) + (smem[2] + smem[3]);
+    // slots past this grid (the sink's buffer is sized for any producer): zero, or stale partials
+    // of an earlier producer would enter the norm
+    if (blockIdx.x == 0)
+      for (int s = p.tiles_m * p.tiles_n + tid; s < p.part_n; s += NT) p.part[s] = 0.f;
+  }
+}
+
+// Sums the ks slice partials of one 128 x 128 tile in slice order and applies the epilogue
+// (accumulate, residual, the tile's sum-of-squares partial), as gemm_f32_kernel's.
+template <bool RES, bool PART>
+__global__ __launch_bounds__(NT) void f32_splitk_reduce(F32Args p) {
+  __shared__ float red[NT / 64];
+  const int tid = threadIdx.x;
+  const int tm = blockIdx.x % p.tiles_m, tn = blockIdx.x / p.tiles_m;
+  const long mn = (long)p.M * p.N;
+  float sq = 0.f;
+  for (int e = tid; e < BM * BN; e += NT) {
+    const int m = tm * BM + e / BN, n = tn * BN + e % BN;
+    if (m >= p.M || n >= p.N) continue;
+    const float* w = p.ws + (long)m * p.N + n;
+    float x = w[0];
+    for (int s = 1; s < p.ks; ++s) x += w[s * mn];
+    float* cp = p.c + (long)m * p.ldc + n;
+    if (p.acc) x += *cp;
+    if constexpr (RES) x += p.r[(long)m * p.ldr + n];
+    if constexpr (PART) sq = fmaf(x, x, sq);
+    *cp = x;
+  }
+  if constexpr (PART) {
+    sq = wave_sum(sq);
+    if ((tid & 63) == 0) red[tid >> 6] = sq;
+    __syncthreads();
+    if (tid == 0) p.part[tn * p.tiles_m + tm] = (red[0] + red[1]) + (red[2] + red[3]);
+    if (blockIdx.x == 0)
+      for (int s = p.tiles_m * p.tiles_n + tid; s < p.part_n; s += NT) p.part[s] = 0.f;
+  }
+}
+
+// K slices: -1 automatic, 0 / 1 none, > 1 forced where K allows (gemm_f32_set_splitk, for A/B)
+int g_f32_splitk = -1;
+
+// (every slice non-empty: ceil(nk / ceil(nk / s)) slices of ceil(nk / s) K-tiles, the last shorter)
+int f32_slices(int ntile, int nk_all) {
+  int s = 1;
+  if (g_f32_splitk >= 0) {
+    s = std::max(1, std::min(g_f32_splitk, nk_all));
+  } else if (ntile < 256) {  // less than a tile per CU: enough workgroups for two per CU, slices of
+    for (int c : {2, 3, 4, 6, 8})  // at least 8 K-tiles (256 deep)
+      if ((long)ntile * c <= 512 && nk_all / c >= 8) s = c;
+  }
+  const int per = (nk_all + s - 1) / s;
+  return (nk_all + per - 1) / per;
+}
+
+template <bool AT, bool BT>
+void launch_lay(const F32Args& p, bool res, bool part, hipStream_t st) {
+  const dim3 g(p.tiles_m * p.tiles_n * p.ks), b(NT);
+  if (p.ks > 1) {  // slices write raw partials: one instantiation, then the reduction's epilogue
+    hipLaunchKernelGGL((gemm_f32_kernel<AT, BT, false, false>), g, b, 0, st, p);
+    const dim3 gr(p.tiles_m * p.tiles_n);
+    if (res && part)
+      hipLaunchKernelGGL((f32_splitk_reduce<true, true>), gr, b, 0, st, p);
+    else if (res)
+      hipLaunchKernelGGL((f32_splitk_reduce<true, false>), gr, b, 0, st, p);
+    else if (part)
+      hipLaunchKernelGGL((f32_splitk_reduce<false, true>), gr, b, 0, st, p);
+    else
+      hipLaunchKernelGGL((f32_splitk_reduce<false, false>), gr, b, 0, st, p);
+    return;
+  }
+  if (res && part)
+    hipLaunchKernelGGL((gemm_f32_kernel<AT, BT, true, true>), g, b, 0, st, p);
+  else if (res)
+    hipLaunchKernelGGL((gemm_f32_kernel<AT, BT, true, false>), g, b, 0, st, p);
+  else if (part)
+    hipLaunchKernelGGL((gemm_f32_kernel<AT, BT, false, true>), g, b, 0, st, p);
+  else
+    hipLaunchKernelGGL((gemm_f32_kernel<AT, BT, false, false>), g, b, 0, st, p);
+}
+
+long ld_of(const at::Tensor& t, const char* name) {
+  TORCH_CHECK(t.dim() == 2 && t.stride(1) == 1, "gemm_f32: ", name, " must be 2-D with unit column stride");
+  TORCH_CHECK(t.stride(0) % 4 == 0 && reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0,
+              "gemm_f32: ", name, " rows must be 16-byte aligned");
+  return t.stride(0);
+}
+
+}  // namespace
+
+// C[M, N] (+)= A B^T over K (layouts above), fp32. K % 32 == 0; a k-major (transposed) operand needs
+// its row count % 4 == 0. out: written (or accumulated) in place and returned; part: per-tile
+// sums of squares of the stored C (>= ceil(M / 128) * ceil(N / 128) slots); residual: [M, N] added.
+at::Tensor gemm_f32(const at::Tensor& a, bool a_t, const at::Tensor& b, bool b_t, int64_t M, int64_t N, int64_t K,
+                    const std::optional<at::Tensor>& out, bool accumulate, const std::optional<at::Tensor>& part,
+                    const std::optional<at::Tensor>& residual) {
+  FT_CHECK_CUDA(a);
+  FT_CHECK_F32(a);
+  FT_CHECK_F32(b);
+  TORCH_CHECK(M > 0 && N > 0 && K > 0 && K % BK == 0, "gemm_f32: K must be a positive multiple of 32");
+  TORCH_CHECK(a.size(0) == (a_t ? K : M) && a.size(1) == (a_t ? M : K), "gemm_f32: a shape");
+  TORCH_CHECK(b.size(0) == (b_t ? K : N) && b.size(1) == (b_t ? N : K), "gemm_f32: b shape");
+  TORCH_CHECK(!a_t || M % 4 == 0, "gemm_f32: a k-major A needs M % 4 == 0");
+  TORCH_CHECK(!b_t || N % 4 == 0, "gemm_f32: a k-major B needs N % 4 == 0");
+  const at::DeviceGuard guard(a.device());
+  F32Args p{};
+  p.a = cptr<float>(a);
+  p.b = cptr<float>(b);
+  p.lda = ld_of(a, "a");
+  p.ldb = ld_of(b, "b");
+  at::Tensor c;
+  if (out.has_value() && out->defined()) {
+    c = *out;
+    FT_CHECK_F32(c);
+    TORCH_CHECK(c.size(0) == M && c.size(1) == N, "gemm_f32: out shape");
+    p.ldc = ld_of(c, "out");
+  } else {
+    TORCH_CHECK(!accumulate, "gemm_f32: accumulate needs out");
+    c = at::empty({M, N}, a.options());
+    p.ldc = N;
+  }
+  p.c = mptr<float>(c);
+  p.acc = accumulate ? 1 : 0;
+  p.M = (int)M;
+  p.N = (int)N;
+  p.K = (int)K;
+  p.tiles_m = (int)((M + BM - 1) / BM);
+  p.tiles_n = (int)((N + BN - 1) / BN);
+  const bool res = residual.has_value() && residual->defined();
+  if (res) {
+    FT_CHECK_F32((*residual));
+    TORCH_CHECK(residual->size(0) == M && residual->size(1) == N, "gemm_f32: residual shape");
+    p.r = cptr<float>(*residual);
+    p.ldr = ld_of(*residual, "residual");
+  }
+  const bool pt = part.has_value() && part->defined();
+  if (pt) {
+    FT_CHECK_F32((*part));
+    FT_CHECK_CONTIG((*part));
+    TORCH_CHECK(part->numel() >= (long)p.tiles_m * p.tiles_n, "gemm_f32: part holds ", part->numel(),
+                " partials, need ", (long)p.tiles_m * p.tiles_n);
+    p.part = mptr<float>(*part);
+    p.part_n = (int)part->numel();
+  }
+  p.ks = f32_slices(p.tiles_m * p.tiles_n, p.K / BK);
+  at::Tensor ws;
+  if (p.ks > 1) {
+    ws = at::empty({(long)p.ks, M, N}, a.options());
+    p.ws = mptr<float>(ws);
+  }
+  const hipStream_t st = ft_stream();
+  if (a_t) {
+    if (b_t) launch_lay<true, true>(p, res, pt, st); else launch_lay<true, false>(p, res, pt, st);
+  } else {
+    if (b_t) launch_lay<false, true>(p, res, pt, st); else launch_lay<false, false>(p, res, pt, st);
+  }
+  FT_LAUNCH_CHECK();
+  return c;
+}
+
+void gemm_f32_set_splitk(int64_t s) { g_f32_splitk = (int)s; }
+int64_t gemm_f32_slices(int64_t M, int64_t N, int64_t K) {
+  return f32_slices((int)(((M + BM - 1) / BM) * ((N + BN - 1) / BN)), (int)(K / BK));
+}
+
+TORCH_LIBRARY_FRAGMENT(ftamd, m) {
+  m.def("gemm_f32_set_splitk(int s) -> ()", &gemm_f32_set_splitk);
+  m.def("gemm_f32_slices(int M, int N, int K) -> int", &gemm_f32_slices);
+  m.def(
+      "gemm_f32(Tensor a, bool a_t, Tensor b, bool b_t, int M, int N, int K, Tensor(a!)? out=None, "
+      "bool accumulate=False, Tensor(b!)? part=None, Tensor? residual=None) -> Tensor",
+      &gemm_f32);
+}

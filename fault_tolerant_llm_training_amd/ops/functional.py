@@ -4,12 +4,12 @@ GPU tensors run the hand-written gfx950 kernels in ``csrc/kernels`` (loaded by
 :func:`fault_tolerant_llm_training_amd._native.kernels`, which raises if the
 library is missing). Every bf16 / fp16 GEMM of the Llama-3-8B and GPT-2 presets runs on the
 hand-written w4 MFMA kernel (``csrc/kernels/gemm_w4.h``; the routing table per preset is pinned by
-``tests/test_routing_cpu.py``); hipBLASLt (``torch.mm`` / ``torch.addmm``) remains for the fp32 /
-fp64 models (the MFMA kernels are 16-bit: ``--model-dtype fp32`` logs that fallback once at
-startup) and for shapes no w4 tile fits.
+``tests/test_routing_cpu.py``); the fp32 models' GEMMs run on the hand-written fp32 MFMA kernel
+(``csrc/kernels/gemm_f32.hip``, v_mfma_f32_16x16x4_f32); hipBLASLt (``torch.mm`` / ``torch.addmm``)
+remains for fp64 models and for shapes no hand-written tile fits.
 Model dtypes (``--model-dtype``): bf16 (every kernel), fp16 (every kernel; the MFMA GEMM and
 flash kernels in their fp16 variants), fp32 (the element-wise / reduction kernels in fp32,
-fp32 attention kernels, fp32 hipBLASLt GEMMs).
+fp32 attention kernels, the fp32 MFMA GEMM).
 CPU tensors run a pure-PyTorch reference of the same math (the CPU backend for
 the gloo tests); its backward recomputes the forward under autograd.
 
@@ -53,6 +53,23 @@ _BLAS_ONLY = os.environ.get("FT_GEMM_BLAS", "0") == "1"
 _W4_FWD = True   # forward products on w4 (A/B: set_w4_fwd)
 _W4_BWD = os.environ.get("FT_W4_BWD", "1") != "0"  # backward products on w4 (A/B: the hipBLASLt backward)
 _W4_DTYPES = (torch.bfloat16, torch.float16)  # bf16 / fp16 MFMA variants of the kernel
+# fp32 models: the fp32 MFMA kernel (gemm_f32.hip) for every product it takes (K % 32; a k-major
+# operand with rows % 4); FT_F32_MFMA=0 / set_f32_mfma(False): hipBLASLt (A/B)
+_F32_MFMA = os.environ.get("FT_F32_MFMA", "1") != "0"
+
+
+def set_f32_mfma(on: bool) -> None:
+    global _F32_MFMA
+    _F32_MFMA = bool(on)
+
+
+def f32_route(M: int, N: int, K: int, a_t: bool, b_t: bool, *ts) -> bool:
+    """C[M, N] over K on the fp32 MFMA kernel? fp32 CUDA operands, K % 32, a k-major A with
+    M % 4 / B with N % 4 (float4 rows), 16-B aligned rows."""
+    if _BLAS_ONLY or not _F32_MFMA or not all(t.is_cuda and t.dtype == torch.float32 for t in ts):
+        return False
+    return K % 32 == 0 and K > 0 and (not a_t or M % 4 == 0) and (not b_t or N % 4 == 0) and all(
+        t.shape[-1] % 4 == 0 for t in ts)
 # Workgroups (output tiles x K slices) a product needs before it goes to the w4 kernel: half the
 # chip. (Tests lower it to drive small shapes through the same paths.)
 _W4_MIN_TILES = 128
@@ -166,6 +183,8 @@ def mm_fwd(x2: torch.Tensor, w: torch.Tensor, residual: Optional[torch.Tensor] =
         return kernels().gemm_nt_s(x2.contiguous(), w, None, res, 1)
     if _w4_fwd_ok(T, N, K, x2, w):
         return kernels().gemm_nt_w4(x2.contiguous(), w, None, res, 0, 0)
+    if w.is_contiguous() and f32_route(T, N, K, False, False, x2, w):
+        return kernels().gemm_f32(x2.contiguous(), False, w, False, T, N, K, None, False, None, res)
     if residual is None:
         return torch.mm(x2, w.t())
     return torch.addmm(residual.reshape(T, N), x2, w.t())
@@ -184,6 +203,8 @@ def mm_dx(dy2: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None
     K = w.shape[1]
     if _w4_dx_ok(T, K, N, dy2, w) and (out is None or out.is_contiguous()):
         return kernels().gemm_w4_ex(dy2.contiguous(), False, w, True, T, K, N, out, False, None, 0, 0)
+    if w.is_contiguous() and (out is None or out.is_contiguous()) and f32_route(T, K, N, False, True, dy2, w):
+        return kernels().gemm_f32(dy2.contiguous(), False, w, True, T, K, N, out, False, None, None)
     if out is not None:
         return torch.mm(dy2, w, out=out)
     return torch.mm(dy2, w)
@@ -192,6 +213,23 @@ def mm_dx(dy2: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None
 def _w4_dw_ok(T: int, N: int, K: int, dy2: torch.Tensor, x2: torch.Tensor) -> bool:
     return (_W4_BWD and dy2.is_contiguous() and x2.is_contiguous()
             and w4_route(N, K, T, True, True, dy2, x2))
+
+
+def _f32_dw_ok(T: int, N: int, K: int, dy2: torch.Tensor, x2: torch.Tensor) -> bool:
+    return dy2.is_contiguous() and x2.is_contiguous() and f32_route(N, K, T, True, True, dy2, x2)
+
+
+def _f32_dw(dy2, x2, out, accumulate: bool, sink: Optional[GradSink]):
+    """dW = dy2^T x2 on the fp32 MFMA kernel (k-major operands read as stored), (+)= into ``out``,
+    with the sink's norm partials (of the stored values, as the w4 dW epilogue) when ``sink`` is
+    given: the product that writes the sink's final gradient."""
+    T, N = dy2.shape
+    K = x2.shape[1]
+    part = sink.part if sink is not None else None
+    r = kernels().gemm_f32(dy2, True, x2, True, N, K, T, out, accumulate, part, None)
+    if part is not None:
+        sink.sq_done = True
+    return r
 
 
 def weight_grad(dy2: torch.Tensor, x2: torch.Tensor, sink: Optional[GradSink]):
@@ -206,6 +244,12 @@ def weight_grad(dy2: torch.Tensor, x2: torch.Tensor, sink: Optional[GradSink]):
         kernels().gemm_w4_ex(dy2, True, x2, True, N, K, T, sink.buf.view(N, K), sink.accumulate, sink.part, 0, 0)
         if sink.part is not None:
             sink.sq_done = True
+        sink.ready()
+        return None
+    if _f32_dw_ok(T, N, K, dy2, x2):
+        if sink is None:
+            return _f32_dw(dy2, x2, None, False, None)
+        _f32_dw(dy2, x2, sink.buf.view(N, K), sink.accumulate, sink)
         sink.ready()
         return None
     if sink is not None:
@@ -671,6 +715,9 @@ def _dw_into(out: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor, accumulate:
         kernels().gemm_w4_ex(dy2, True, x2, True, N, K, T, out, accumulate, part, 0, 0)
         if part is not None:
             sink.sq_done = True
+        return
+    if _f32_dw_ok(T, N, K, dy2, x2) and out.is_contiguous():
+        _f32_dw(dy2, x2, out, accumulate, sink)
         return
     if accumulate:
         out.addmm_(dy2.t(), x2)

@@ -25,7 +25,7 @@ def _w4_name(M, N, K, a_t, b_t):
 def routing_table(margs, dtype, tokens: int = 2048, cuda: bool = True) -> dict:
     """{product: kernel} for one transformer layer and the LM head of ``margs`` at ``tokens`` rows:
     "w4 <tile width>[ xS]" (S = K slices), "w4 qkv+rope", "w4 swiglu", "w4 swiglu-bwd", "gemm_s",
-    or "hipBLASLt"."""
+    "f32 mfma" (fp32 models: csrc/kernels/gemm_f32.hip), or "hipBLASLt"."""
     T, D, V = tokens, margs.dim, margs.vocab_size
     hd, Hq, Hkv, Fh = margs.head_dim, margs.n_heads, margs.kv_heads, margs.ffn_hidden
     W = (Hq + 2 * Hkv) * hd
@@ -39,13 +39,17 @@ def routing_table(margs, dtype, tokens: int = 2048, cuda: bool = True) -> dict:
             return "gemm_s"
         if Fx._w4_fwd_ok(Tn, N, K, xx, w):
             return _w4_name(Tn, N, K, False, False)
-        return "hipBLASLt"
+        return "f32 mfma" if Fx.f32_route(Tn, N, K, False, False, xx, w) else "hipBLASLt"
 
     def dx(Tn, K, N, w):
-        return _w4_name(Tn, K, N, False, True) if Fx._w4_dx_ok(Tn, K, N, sp(Tn, N), w) else "hipBLASLt"
+        if Fx._w4_dx_ok(Tn, K, N, sp(Tn, N), w):
+            return _w4_name(Tn, K, N, False, True)
+        return "f32 mfma" if Fx.f32_route(Tn, K, N, False, True, sp(Tn, N), w) else "hipBLASLt"
 
     def dw(Tn, N, K):
-        return _w4_name(N, K, Tn, True, True) if Fx._w4_dw_ok(Tn, N, K, sp(Tn, N), sp(Tn, K)) else "hipBLASLt"
+        if Fx._w4_dw_ok(Tn, N, K, sp(Tn, N), sp(Tn, K)):
+            return _w4_name(N, K, Tn, True, True)
+        return "f32 mfma" if Fx._f32_dw_ok(Tn, N, K, sp(Tn, N), sp(Tn, K)) else "hipBLASLt"
 
     t = {}
     t["qkv fwd"] = "w4 qkv+rope" if A._qkv_rope_ok(x, wqkv, hd) else fwd(x, wqkv)

@@ -90,14 +90,15 @@ def set_fused_sumsq(on: bool) -> None:
 
 
 def sink_partials(numel: int, ndim: int, shape=None) -> int:
-    """Partial slots a sink's producers may write: one per w4 output tile (>= 256 x 128 elements,
-    a tail tile of the dW layout covering fewer: ceil(rows / 256) x ceil(cols / 128) bounds them)
-    of a 2-D weight, one per 32 columns of a 1-D one; also the grid of the fallback sumsq pass."""
+    """Partial slots a sink's producers may write: one per output tile of a 2-D weight (w4: 256 x
+    >= 128, a tail tile of the dW layout covering fewer; the fp32 MFMA GEMM: 128 x 128 -- so
+    ceil(rows / 128) x ceil(cols / 128) bounds both), one per 32 columns of a 1-D one; also the grid
+    of the fallback sumsq pass."""
     if ndim <= 1:
         return max(1, (numel + 31) // 32)
     n = max(1, (numel + 32767) // 32768)
     if shape is not None and len(shape) == 2:
-        n = max(n, -(-int(shape[0]) // 256) * -(-int(shape[1]) // 128))
+        n = max(n, -(-int(shape[0]) // 128) * -(-int(shape[1]) // 128))
     return n
 
 

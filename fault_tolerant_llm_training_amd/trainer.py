@@ -224,10 +224,11 @@ def train(args) -> int:
         # (rocBLAS dgemm, reference attention): correct, not fast
         logger.info("--model-dtype fp64 on the GPU: composed PyTorch ops (the HIP kernels cover bf16/fp16/fp32)")
     if model_dtype == torch.float32:
-        # the reference accepts fp32 (utils.py:14-19); the hand-written MFMA GEMM is 16-bit, so an
-        # fp32 model's GEMMs are the vendor's (ops/functional.py routing; tests/test_routing_cpu.py)
-        logger.info("--model-dtype fp32: GEMMs on hipBLASLt (torch.mm) -- the hand-written w4 MFMA GEMM is "
-                    "bf16/fp16; norms, RoPE, SwiGLU, attention, cross-entropy and AdamW keep their fp32 HIP kernels")
+        # the reference accepts fp32 (utils.py:14-19); the w4 GEMM is 16-bit, so an fp32 model's GEMMs
+        # take the fp32 MFMA kernel (ops/functional.py f32_route; tests/test_routing_cpu.py)
+        logger.info("--model-dtype fp32: GEMMs on the fp32 MFMA kernel (gemm_f32, v_mfma_f32_16x16x4_f32; "
+                    "hipBLASLt where K % 32 != 0) -- the w4 GEMM is bf16/fp16; norms, RoPE, SwiGLU, attention, "
+                    "cross-entropy and AdamW run their fp32 HIP kernels")
     torch.manual_seed(args.seed)
     from .ops.attention import set_deterministic
 

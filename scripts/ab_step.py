@@ -30,6 +30,7 @@ Knobs toggled between timing windows (alternating rounds, so box and clock drift
           instead of re-staging the last K-tile (round 6)
   remainder — a 1.5-round dW grid (the 8B qkv dW) as a full round of 256-wide tiles plus the
           remaining rows at the 128-wide tile (round 6)
+  f32mfma — (--dtype fp32) the fp32 model's GEMMs on the fp32 MFMA kernel instead of hipBLASLt
 Usage: python scripts/ab_step.py [--steps 8] [--rounds 3] [--configs gemm,dw ...]
 """
 from __future__ import annotations
@@ -55,6 +56,7 @@ def main():
     ap.add_argument("--steps", type=int, default=8)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--knobs", default="splitk")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp16", "fp32"])
     a = ap.parse_args()
 
     from fault_tolerant_llm_training_amd.data.synthetic import SyntheticTokens
@@ -67,7 +69,8 @@ def main():
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     margs = model_args_for(a.model, vocab_size=a.vocab_size, seq_len=a.seq_len)
-    model = build_model(margs, dev, torch.bfloat16, seed=1234)
+    dt = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}[a.dtype]
+    model = build_model(margs, dev, dt, seed=1234)
     red = GradReducer(model.flat, model.sinks_in_backward_order())  # bench.py's default buckets
     opt = FlatAdamW(model.parameters(), model.flat, lr=5e-5, max_grad_norm=1.0, reducer=red)
     model.gate = opt.gate
@@ -123,6 +126,7 @@ def main():
                "adamw_serial": lambda on: serial_adamw.__setitem__(0, bool(on)),
                "raster": lambda on: (torch.cuda.synchronize(), kernels().gemm_w4_set_group(-1 if on else 0)),
                "deadzero": lambda on: (torch.cuda.synchronize(), kernels().gemm_w4_set_deadzero(1 if on else 0)),
+               "f32mfma": lambda on: (torch.cuda.synchronize(), Fx.set_f32_mfma(on)),
                "remainder": lambda on: (torch.cuda.synchronize(), kernels().gemm_w4_set_remainder(1 if on else 0))}
     configs = list(itertools.product([False, True], repeat=len(knobs)))
 
@@ -147,7 +151,7 @@ def main():
         name = " ".join(f"{k}={'on' if on else 'off'}" for k, on in zip(knobs, cfg))
         best = min(res[cfg])
         print(f"[ab] {name:24s} best {best:7.2f} ms/step  median {sorted(res[cfg])[len(res[cfg]) // 2]:7.2f}  "
-              f"{base / best:.3f}x vs all-off  ({2048 * 1000 / best:.0f} tok/s)", flush=True)
+              f"{base / best:.3f}x vs all-off  ({a.seq_len * 1000 / best:.0f} tok/s)", flush=True)
     loss = step()
     torch.cuda.synchronize()
     print(f"[ab] final loss {float(loss):.4f}", flush=True)

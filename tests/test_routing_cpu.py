@@ -4,7 +4,8 @@ each product of the step takes, so a routing change is a visible test change:
 
 * Llama-3-8B bf16 / fp16: every product on the hand-written w4 kernel -- none on hipBLASLt (the
   deep-reduction dX products with a K split);
-* fp32 models and CPU tensors: hipBLASLt / the composed path (the MFMA kernels are 16-bit);
+* fp32 models: every product on the hand-written fp32 MFMA kernel (gemm_f32.hip); CPU tensors:
+  the composed path;
 * GPT-2-sized presets at one sequence: every product on w4 too (round 6: K splits for the small
   grids, a tail tile for V % 256), none on hipBLASLt.
 """
@@ -33,10 +34,15 @@ def test_llama8b_every_product_on_w4(dtype):
 
 
 @pytest.mark.parametrize("preset", ["llama3-8b", "gpt2-small", "gpt2-medium"])
-def test_fp32_and_cpu_take_no_mfma_gemm(preset):
+def test_fp32_takes_the_f32_mfma_gemm_and_cpu_the_composed_path(preset, monkeypatch):
+    """fp32 models (reference utils.py:14-19): every product of the layer and the LM head on the fp32
+    MFMA kernel (round 6; before: hipBLASLt); set_f32_mfma(False) / FT_F32_MFMA=0 restores hipBLASLt."""
     a = model_args_for(preset, vocab_size=50304 if preset != "llama3-8b" else 131072, seq_len=2048)
-    assert set(routing_table(a, torch.float32).values()) == {"hipBLASLt"}
+    assert set(routing_table(a, torch.float32).values()) == {"f32 mfma"}
     assert set(routing_table(a, torch.bfloat16, cuda=False).values()) == {"hipBLASLt"}
+    assert set(routing_table(a, torch.float64).values()) == {"hipBLASLt"}
+    monkeypatch.setattr(Fx, "_F32_MFMA", False)
+    assert set(routing_table(a, torch.float32).values()) == {"hipBLASLt"}
 
 
 @pytest.mark.parametrize("preset,vocab", [("gpt2-small", 50304), ("gpt2-small", 131072),
@@ -75,10 +81,9 @@ def test_blas_only_knob(monkeypatch):
     assert A._qkv_rope_ok is not None
 
 
-def test_fp32_model_logs_the_hipblaslt_fallback_once(tmp_path):
-    """--model-dtype fp32 (reference utils.py:14-19): the hand-written MFMA GEMM is 16-bit, so the
-    GEMMs of an fp32 model are hipBLASLt's -- a documented deviation, logged once at startup, never
-    silent."""
+def test_fp32_model_logs_its_gemm_kernel_once(tmp_path):
+    """--model-dtype fp32 (reference utils.py:14-19): the w4 GEMM is 16-bit, so the GEMMs of an fp32
+    model take the fp32 MFMA kernel (hipBLASLt where K % 32 != 0) -- logged once at startup."""
     import os
 
     from helpers import TINY, run_train, write_fake_sbatch
@@ -88,10 +93,10 @@ def test_fp32_model_logs_the_hipblaslt_fallback_once(tmp_path):
     rc, out = run_train(d, "4101", TINY + ["--synthetic-data", "--vocab-size", "256", "--model-dtype", "fp32",
                                            "--training-steps", "3", "--checkpoint-path", os.path.join(d, "ck")])
     assert rc == 0 and "Training completed" in out, out[-2000:]
-    assert out.count("--model-dtype fp32: GEMMs on hipBLASLt") == 1, out[-2000:]
+    assert out.count("--model-dtype fp32: GEMMs on the fp32 MFMA kernel") == 1, out[-2000:]
     rc, out = run_train(d, "4102", TINY + ["--synthetic-data", "--vocab-size", "256", "--training-steps", "2",
                                            "--checkpoint-path", os.path.join(d, "ck")])
-    assert rc == 0 and "GEMMs on hipBLASLt" not in out
+    assert rc == 0 and "--model-dtype fp32" not in out
 
 
 def test_qkv_rope_min_k_knob(monkeypatch):
