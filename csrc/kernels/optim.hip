@@ -18,6 +18,8 @@
 // ~8e9 elements instead of ~300-tensor foreach chains.
 #include "torch_utils.h"
 
+#include <vector>
+
 #include <cstdlib>
 
 namespace {
@@ -295,7 +297,24 @@ void norm_finish_(const at::Tensor& partial, const at::Tensor& stats, double max
   FT_LAUNCH_CHECK();
 }
 
+// A stream whose kernels dispatch only to every `stride`-th CU (hipExtStreamCreateWithCUMask), for
+// confining the optimizer's memory-bound AdamW launches to a slice of the chip while the next
+// forward's GEMMs keep the rest (scripts/ab_step.py knob cumask). Returns the hipStream_t as an
+// integer for torch.cuda.ExternalStream; the stream lives for the process.
+int64_t cu_masked_stream(int64_t stride, int64_t phase) {
+  TORCH_CHECK(stride >= 1 && phase >= 0 && phase < stride, "cu_masked_stream: 0 <= phase < stride");
+  int dev = 0, ncu = 0;
+  FT_HIP_CHECK(hipGetDevice(&dev));
+  FT_HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+  std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+  for (int c = (int)phase; c < ncu; c += (int)stride) mask[c / 32] |= 1u << (c % 32);
+  hipStream_t st = nullptr;
+  FT_HIP_CHECK(hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()));
+  return reinterpret_cast<int64_t>(st);
+}
+
 TORCH_LIBRARY_FRAGMENT(ftamd, m) {
+  m.def("cu_masked_stream(int stride, int phase=0) -> int", &cu_masked_stream);
   m.def("sumsq_into_(Tensor grad, Tensor(a!) partial) -> ()", &sumsq_into_);
   m.def("norm_finish_(Tensor partial, Tensor(a!) stats, float max_norm) -> ()", &norm_finish_);
   m.def("grad_norm_(Tensor grad, Tensor(a!) stats, float max_norm) -> ()", &grad_norm_);

@@ -30,6 +30,8 @@ Knobs toggled between timing windows (alternating rounds, so box and clock drift
           instead of re-staging the last K-tile (round 6)
   remainder — a 1.5-round dW grid (the 8B qkv dW) as a full round of 256-wide tiles plus the
           remaining rows at the 128-wide tile (round 6)
+  cumask — the optimizer side stream (norm + AdamW) confined to every 4th CU (hipExtStreamCreateWithCUMask)
+  cumask2 — ... to every 2nd CU
   f32mfma — (--dtype fp32) the fp32 model's GEMMs on the fp32 MFMA kernel instead of hipBLASLt
 Usage: python scripts/ab_step.py [--steps 8] [--rounds 3] [--configs gemm,dw ...]
 """
@@ -128,6 +130,17 @@ def main():
                "deadzero": lambda on: (torch.cuda.synchronize(), kernels().gemm_w4_set_deadzero(1 if on else 0)),
                "f32mfma": lambda on: (torch.cuda.synchronize(), Fx.set_f32_mfma(on)),
                "remainder": lambda on: (torch.cuda.synchronize(), kernels().gemm_w4_set_remainder(1 if on else 0))}
+    side0 = red.side
+    masked = {}
+
+    def set_cumask(stride, on):
+        torch.cuda.synchronize()
+        if on and stride not in masked:
+            masked[stride] = torch.cuda.ExternalStream(kernels().cu_masked_stream(stride, 0), device=dev)
+        red.side = masked[stride] if on else side0
+
+    setters["cumask"] = lambda on: set_cumask(4, on)
+    setters["cumask2"] = lambda on: set_cumask(2, on)
     configs = list(itertools.product([False, True], repeat=len(knobs)))
 
     def apply(cfg):
