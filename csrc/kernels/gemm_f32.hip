@@ -237,33 +237,67 @@ __global__ __launch_bounds__(NT, 2) void gemm_f32_kernel(F32Args p) {
 }
 
 // Sums the ks slice partials of one 128 x 128 tile in slice order and applies the epilogue
-// (accumulate, residual, the tile's sum-of-squares partial), as gemm_f32_kernel's.
+// (accumulate, residual, the tile's sum-of-squares partial), as gemm_f32_kernel's. 1024 threads
+// per tile (the split grids have few tiles: 96 at the GPT-2 sizes), float4 when the rows allow.
+constexpr int RT = 1024;
+
 template <bool RES, bool PART>
-__global__ __launch_bounds__(NT) void f32_splitk_reduce(F32Args p) {
-  __shared__ float red[NT / 64];
+__global__ __launch_bounds__(RT) void f32_splitk_reduce(F32Args p) {
+  __shared__ float red[RT / 64];
   const int tid = threadIdx.x;
   const int tm = blockIdx.x % p.tiles_m, tn = blockIdx.x / p.tiles_m;
   const long mn = (long)p.M * p.N;
+  const bool vec = (p.N % 4 == 0) && (p.ldc % 4 == 0) && (!RES || p.ldr % 4 == 0);  // uniform
   float sq = 0.f;
-  for (int e = tid; e < BM * BN; e += NT) {
-    const int m = tm * BM + e / BN, n = tn * BN + e % BN;
-    if (m >= p.M || n >= p.N) continue;
-    const float* w = p.ws + (long)m * p.N + n;
-    float x = w[0];
-    for (int s = 1; s < p.ks; ++s) x += w[s * mn];
-    float* cp = p.c + (long)m * p.ldc + n;
-    if (p.acc) x += *cp;
-    if constexpr (RES) x += p.r[(long)m * p.ldr + n];
-    if constexpr (PART) sq = fmaf(x, x, sq);
-    *cp = x;
+  if (vec) {
+#pragma unroll
+    for (int q = 0; q < BM * BN / 4 / RT; ++q) {
+      const int e = q * RT + tid;
+      const int m = tm * BM + e / (BN / 4), n = tn * BN + 4 * (e % (BN / 4));
+      if (m >= p.M || n >= p.N) continue;
+      const float* w = p.ws + (long)m * p.N + n;
+      float4 x = *reinterpret_cast<const float4*>(w);
+      for (int s = 1; s < p.ks; ++s) {
+        const float4 y = *reinterpret_cast<const float4*>(w + s * mn);
+        x.x += y.x; x.y += y.y; x.z += y.z; x.w += y.w;
+      }
+      float4* cp = reinterpret_cast<float4*>(p.c + (long)m * p.ldc + n);
+      if (p.acc) {
+        const float4 c0 = *cp;
+        x.x += c0.x; x.y += c0.y; x.z += c0.z; x.w += c0.w;
+      }
+      if constexpr (RES) {
+        const float4 r = *reinterpret_cast<const float4*>(p.r + (long)m * p.ldr + n);
+        x.x += r.x; x.y += r.y; x.z += r.z; x.w += r.w;
+      }
+      if constexpr (PART) sq = fmaf(x.w, x.w, fmaf(x.z, x.z, fmaf(x.y, x.y, fmaf(x.x, x.x, sq))));
+      *cp = x;
+    }
+  } else {
+    for (int e = tid; e < BM * BN; e += RT) {
+      const int m = tm * BM + e / BN, n = tn * BN + e % BN;
+      if (m >= p.M || n >= p.N) continue;
+      const float* w = p.ws + (long)m * p.N + n;
+      float x = w[0];
+      for (int s = 1; s < p.ks; ++s) x += w[s * mn];
+      float* cp = p.c + (long)m * p.ldc + n;
+      if (p.acc) x += *cp;
+      if constexpr (RES) x += p.r[(long)m * p.ldr + n];
+      if constexpr (PART) sq = fmaf(x, x, sq);
+      *cp = x;
+    }
   }
   if constexpr (PART) {
     sq = wave_sum(sq);
     if ((tid & 63) == 0) red[tid >> 6] = sq;
     __syncthreads();
-    if (tid == 0) p.part[tn * p.tiles_m + tm] = (red[0] + red[1]) + (red[2] + red[3]);
+    if (tid == 0) {
+      float t = 0.f;
+      for (int w = 0; w < RT / 64; ++w) t += red[w];  // fixed order
+      p.part[tn * p.tiles_m + tm] = t;
+    }
     if (blockIdx.x == 0)
-      for (int s = p.tiles_m * p.tiles_n + tid; s < p.part_n; s += NT) p.part[s] = 0.f;
+      for (int s = p.tiles_m * p.tiles_n + tid; s < p.part_n; s += RT) p.part[s] = 0.f;
   }
 }
 
@@ -288,15 +322,15 @@ void launch_lay(const F32Args& p, bool res, bool part, hipStream_t st) {
   const dim3 g(p.tiles_m * p.tiles_n * p.ks), b(NT);
   if (p.ks > 1) {  // slices write raw partials: one instantiation, then the reduction's epilogue
     hipLaunchKernelGGL((gemm_f32_kernel<AT, BT, false, false>), g, b, 0, st, p);
-    const dim3 gr(p.tiles_m * p.tiles_n);
+    const dim3 gr(p.tiles_m * p.tiles_n), br(RT);
     if (res && part)
-      hipLaunchKernelGGL((f32_splitk_reduce<true, true>), gr, b, 0, st, p);
+      hipLaunchKernelGGL((f32_splitk_reduce<true, true>), gr, br, 0, st, p);
     else if (res)
-      hipLaunchKernelGGL((f32_splitk_reduce<true, false>), gr, b, 0, st, p);
+      hipLaunchKernelGGL((f32_splitk_reduce<true, false>), gr, br, 0, st, p);
     else if (part)
-      hipLaunchKernelGGL((f32_splitk_reduce<false, true>), gr, b, 0, st, p);
+      hipLaunchKernelGGL((f32_splitk_reduce<false, true>), gr, br, 0, st, p);
     else
-      hipLaunchKernelGGL((f32_splitk_reduce<false, false>), gr, b, 0, st, p);
+      hipLaunchKernelGGL((f32_splitk_reduce<false, false>), gr, br, 0, st, p);
     return;
   }
   if (res && part)
