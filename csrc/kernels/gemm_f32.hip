@@ -115,6 +115,60 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
+// The epilogue of a K slice's 128 x 128 tile: raw partial (split-K) or C (+)= acc (+ residual), with
+// the tile's sum-of-squares partial through `red` (>= 4 floats of LDS no wave still reads).
+template <bool RES, bool PART>
+__device__ __forceinline__ void epilogue(const F32Args& p, f32x4_t (&acc)[4][4], int slice, int tm, int tn,
+                                         int wm, int wn, int lane, int wid, int tid, float* red) {
+  const int m0 = tm * BM, n0 = tn * BN;
+  // epilogue: acc[i][j][v] = C(m0 + 64 wm + 16 i + 4 (lane / 16) + v, n0 + 64 wn + 16 j + lane % 16)
+  const int g = lane >> 4, r16 = lane & 15;
+  if (p.ks > 1) {  // a slice's raw partial (f32_splitk_reduce applies the epilogue)
+    float* w = p.ws + (long)slice * p.M * p.N;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int m = m0 + wm * 64 + i * 16 + 4 * g + v;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int n = n0 + wn * 64 + j * 16 + r16;
+          if (m < p.M && n < p.N) w[(long)m * p.N + n] = acc[i][j][v];
+        }
+      }
+    return;
+  }
+  float sq = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int m = m0 + wm * 64 + i * 16 + 4 * g + v;
+      if (m >= p.M) continue;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = n0 + wn * 64 + j * 16 + r16;
+        if (n >= p.N) continue;
+        float* cp = p.c + (long)m * p.ldc + n;
+        float x = acc[i][j][v];
+        if (p.acc) x += *cp;
+        if constexpr (RES) x += p.r[(long)m * p.ldr + n];
+        if constexpr (PART) sq = fmaf(x, x, sq);
+        *cp = x;
+      }
+    }
+  if constexpr (PART) {  // one partial per tile, fixed order (deterministic)
+    sq = wave_sum(sq);
+    if (lane == 0) red[wid] = sq;
+    __syncthreads();
+    if (tid == 0) p.part[tn * p.tiles_m + tm] = (red[0] + red[1]) + (red[2] + red[3]);
+    // slots past this grid (the sink's buffer is sized for any producer): zero, or stale partials
+    // of an earlier producer would enter the norm
+    if (blockIdx.x == 0)
+      for (int s = p.tiles_m * p.tiles_n + tid; s < p.part_n; s += NT) p.part[s] = 0.f;
+  }
+}
+
 template <bool AT, bool BT, bool RES, bool PART>
 __global__ __launch_bounds__(NT, 2) void gemm_f32_kernel(F32Args p) {
   __shared__ __attribute__((aligned(16))) float smem[LDS_FLOATS];
@@ -188,52 +242,150 @@ __global__ __launch_bounds__(NT, 2) void gemm_f32_kernel(F32Args p) {
   }
   __syncthreads();  // every wave's last (idle-buffer) reads are done before smem is reused
 
-  // epilogue: acc[i][j][v] = C(m0 + 64 wm + 16 i + 4 (lane / 16) + v, n0 + 64 wn + 16 j + lane % 16)
-  const int g = lane >> 4, r16 = lane & 15;
-  if (p.ks > 1) {  // a slice's raw partial (f32_splitk_reduce applies the epilogue)
-    float* w = p.ws + (long)slice * p.M * p.N;
+  epilogue<RES, PART>(p, acc, slice, tm, tn, wm, wn, lane, wid, tid, smem);
+}
+
+// ---- LDS-DMA form (default): the operands go HBM -> LDS by buffer_load_dwordx4 ... lds, never
+// through VGPRs (a register round trip's returning loads compete with the MFMAs for the register
+// file). 16 KiB images without padding, the bank spread done by the DMA's per-lane source address:
+//   k-contiguous [row][32]: 128-B rows, row r's 16-B slot s holds chunk s ^ (r & 7) (ds_read_b128
+//     fragment reads conflict-free);
+//   k-major [k][128]: 512-B k-rows, k-row k's slot s holds chunk s ^ 4 [k & 4] (lanes 16-31, 4
+//     k-rows further, 16 banks away for ds_read_b32).
+// A wave's DMA instruction fills 1 KiB (piece P = 8 rows / 2 k-rows); 4 + 4 per wave per K-tile.
+// Tails are clamped onto the last valid row (their products only reach C entries never stored);
+// every byte offset stays below 4 GiB (host check; 32-bit buffer offsets).
+constexpr int DIMG = 4096;  // floats per operand image (16 KiB)
+typedef int i32x4_t __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ unsigned lds_u32(const void* q) {
+  return (unsigned)(uintptr_t)((const __attribute__((address_space(3))) char*)q);
+}
+
+__device__ __forceinline__ i32x4_t make_srd(const void* q) {
+  const unsigned long long a = (unsigned long long)q;
+  i32x4_t r;
+  r[0] = __builtin_amdgcn_readfirstlane((int)(unsigned)a);
+  r[1] = __builtin_amdgcn_readfirstlane((int)((unsigned)(a >> 32) & 0xffffu));
+  r[2] = -1;
+  r[3] = 0x00020000;
+  return r;
+}
+
+// 16 B per lane from srd + voff + soff into LDS [sbase + 16 * lane] (m0 = sbase; nothing else in
+// the kernel uses m0; s_mov does not touch SCC)
+__device__ __forceinline__ void dma16(const i32x4_t& srd, unsigned voff, unsigned soff, unsigned sbase) {
+  asm volatile("s_mov_b32 m0, %2\n\tbuffer_load_dwordx4 %0, %1, %3 offen lds"
+               :
+               : "v"(voff), "s"(srd), "s"(sbase), "s"(soff)
+               : "memory");
+}
+
+// per-lane source offsets (bytes, without the K-tile's soff) of the 4 pieces a wave fills
+template <bool RC>
+__device__ __forceinline__ void dma_offsets(long ld, int i0, int rows, int wid, int lane, unsigned (&vo)[4]) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        const int m = m0 + wm * 64 + i * 16 + 4 * g + v;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int n = n0 + wn * 64 + j * 16 + r16;
-          if (m < p.M && n < p.N) w[(long)m * p.N + n] = acc[i][j][v];
-        }
-      }
-    return;
+  for (int q = 0; q < 4; ++q) {
+    const int P = q * 4 + wid;
+    if constexpr (RC) {
+      const int k = 2 * P + (lane >> 5);
+      const int c = (lane & 31) ^ (((k >> 2) & 1) * 4);
+      const int i = min(i0 + 4 * c, rows - 4);
+      vo[q] = (unsigned)(((long)k * ld + i) * 4);
+    } else {
+      const int r = 8 * P + (lane >> 3);
+      const int c = (lane & 7) ^ (r & 7);
+      const int i = min(i0 + r, rows - 1);
+      vo[q] = (unsigned)(((long)i * ld + 4 * c) * 4);
+    }
   }
-  float sq = 0.f;
+}
+
+// f[j] = X(row base + lane % 16, k = 16 c + 4 (lane / 16) + j) from a swizzled image
+template <bool RC>
+__device__ __forceinline__ float4 dfrag(const float* img, int base, int c, int lane) {
+  const int r16 = lane & 15, g = lane >> 4;
+  if constexpr (RC) {
+    const int m = base + r16;
+    const float* q = img + (16 * c + 4 * g) * 128 + ((((m >> 2) ^ ((g & 1) * 4))) << 2) + (m & 3);
+    return make_float4(q[0], q[128], q[256], q[384]);  // (k + 1 .. k + 3 share bit 2 of k: same swizzle)
+  } else {
+    const int r = base + r16;
+    return *reinterpret_cast<const float4*>(img + r * 32 + (((4 * c + g) ^ (r & 7)) << 2));
+  }
+}
+
+template <bool AT, bool BT, bool RES, bool PART>
+__global__ __launch_bounds__(NT, 2) void gemm_f32d_kernel(F32Args p) {
+  __shared__ __attribute__((aligned(1024))) float smem[2 * 2 * DIMG];  // 2 stages x (A, B): 64 KiB
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 1, wn = wid & 1;
+  const int ntile = p.tiles_m * p.tiles_n;
+  const int slice = blockIdx.x / ntile;
+  int tm, tn;
+  tile_of(blockIdx.x - slice * ntile, p.tiles_m, p.tiles_n, tm, tn);
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int nk_all = p.K / BK, per = (nk_all + p.ks - 1) / p.ks;
+  const int kb = slice * per * BK;
+  const int nk = min(per, nk_all - slice * per);
+
+  const i32x4_t srdA = make_srd(p.a), srdB = make_srd(p.b);
+  unsigned voA[4], voB[4];
+  dma_offsets<AT>(p.lda, m0, p.M, wid, lane, voA);
+  dma_offsets<BT>(p.ldb, n0, p.N, wid, lane, voB);
+  // soff of K-tile t: k-major operands advance by BK rows, k-contiguous ones by BK columns
+  const unsigned stA = AT ? (unsigned)(BK * p.lda * 4) : (unsigned)(BK * 4);
+  const unsigned stB = BT ? (unsigned)(BK * p.ldb * 4) : (unsigned)(BK * 4);
+  const unsigned sA0 = AT ? (unsigned)((long)kb * p.lda * 4) : (unsigned)(kb * 4);
+  const unsigned sB0 = BT ? (unsigned)((long)kb * p.ldb * 4) : (unsigned)(kb * 4);
+  const unsigned lds0 = __builtin_amdgcn_readfirstlane(lds_u32(smem));
+  auto issue = [&](int t, int stage) __attribute__((always_inline)) {
+    const unsigned ba = lds0 + (unsigned)(stage * 2 * DIMG * 4), bb = ba + DIMG * 4;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const unsigned piece = (unsigned)((q * 4 + wid) * 1024);
+      dma16(srdA, voA[q], sA0 + t * stA, __builtin_amdgcn_readfirstlane(ba + piece));
+      dma16(srdB, voB[q], sB0 + t * stB, __builtin_amdgcn_readfirstlane(bb + piece));
+    }
+  };
+
+  f32x4_t acc[4][4];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      const int m = m0 + wm * 64 + i * 16 + 4 * g + v;
-      if (m >= p.M) continue;
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  issue(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const float* cur = smem + (kt & 1) * 2 * DIMG;
+    if (kt + 1 < nk) issue(kt + 1, (kt + 1) & 1);  // (uniform) into the stage read last iteration
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int n = n0 + wn * 64 + j * 16 + r16;
-        if (n >= p.N) continue;
-        float* cp = p.c + (long)m * p.ldc + n;
-        float x = acc[i][j][v];
-        if (p.acc) x += *cp;
-        if constexpr (RES) x += p.r[(long)m * p.ldr + n];
-        if constexpr (PART) sq = fmaf(x, x, sq);
-        *cp = x;
+    for (int c = 0; c < BK / 16; ++c) {
+      float4 fa[4], fb[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fa[i] = dfrag<AT>(cur, wm * 64 + i * 16, c, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fb[j] = dfrag<BT>(cur + DIMG, wn * 64 + j * 16, c, lane);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float av = q == 0 ? fa[i].x : q == 1 ? fa[i].y : q == 2 ? fa[i].z : fa[i].w;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float bv = q == 0 ? fb[j].x : q == 1 ? fb[j].y : q == 2 ? fb[j].z : fb[j].w;
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[i][j], 0, 0, 0);
+          }
+        }
       }
     }
-  if constexpr (PART) {  // one partial per tile, fixed order (deterministic)
-    sq = wave_sum(sq);
-    if (lane == 0) smem[wid] = sq;
-    __syncthreads();
-    if (tid == 0) p.part[tn * p.tiles_m + tm] = (smem[0] + smem[1]) + (smem[2] + smem[3]);
-    // slots past this grid (the sink's buffer is sized for any producer): zero, or stale partials
-    // of an earlier producer would enter the norm
-    if (blockIdx.x == 0)
-      for (int s = p.tiles_m * p.tiles_n + tid; s < p.part_n; s += NT) p.part[s] = 0.f;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next K-tile's DMA landed (this wave's) ...
+    __syncthreads();                                   // ... and everyone's; cur is free again
   }
+  epilogue<RES, PART>(p, acc, slice, tm, tn, wm, wn, lane, wid, tid, smem);
 }
 
 // Sums the ks slice partials of one 128 x 128 tile in slice order and applies the epilogue
@@ -317,11 +469,25 @@ int f32_slices(int ntile, int nk_all) {
   return (nk_all + per - 1) / per;
 }
 
+// LDS-DMA form (default) or the register round-trip form (gemm_f32_set_dma, A/B; also taken when an
+// operand exceeds 32-bit buffer offsets)
+int g_f32_dma = 1;
+
 template <bool AT, bool BT>
-void launch_lay(const F32Args& p, bool res, bool part, hipStream_t st) {
+void launch_lay(const F32Args& p, bool res, bool part, bool dma, hipStream_t st) {
   const dim3 g(p.tiles_m * p.tiles_n * p.ks), b(NT);
+  if (dma) {
+    if (p.ks > 1 || (!res && !part))
+      hipLaunchKernelGGL((gemm_f32d_kernel<AT, BT, false, false>), g, b, 0, st, p);
+    else if (res && part)
+      hipLaunchKernelGGL((gemm_f32d_kernel<AT, BT, true, true>), g, b, 0, st, p);
+    else if (res)
+      hipLaunchKernelGGL((gemm_f32d_kernel<AT, BT, true, false>), g, b, 0, st, p);
+    else
+      hipLaunchKernelGGL((gemm_f32d_kernel<AT, BT, false, true>), g, b, 0, st, p);
+  }
   if (p.ks > 1) {  // slices write raw partials: one instantiation, then the reduction's epilogue
-    hipLaunchKernelGGL((gemm_f32_kernel<AT, BT, false, false>), g, b, 0, st, p);
+    if (!dma) hipLaunchKernelGGL((gemm_f32_kernel<AT, BT, false, false>), g, b, 0, st, p);
     const dim3 gr(p.tiles_m * p.tiles_n), br(RT);
     if (res && part)
       hipLaunchKernelGGL((f32_splitk_reduce<true, true>), gr, br, 0, st, p);
@@ -333,6 +499,7 @@ void launch_lay(const F32Args& p, bool res, bool part, hipStream_t st) {
       hipLaunchKernelGGL((f32_splitk_reduce<false, false>), gr, br, 0, st, p);
     return;
   }
+  if (dma) return;
   if (res && part)
     hipLaunchKernelGGL((gemm_f32_kernel<AT, BT, true, true>), g, b, 0, st, p);
   else if (res)
@@ -412,23 +579,28 @@ at::Tensor gemm_f32(const at::Tensor& a, bool a_t, const at::Tensor& b, bool b_t
     ws = at::empty({(long)p.ks, M, N}, a.options());
     p.ws = mptr<float>(ws);
   }
+  // the DMA form's 32-bit buffer offsets: every operand byte within 4 GiB of its base
+  const auto fits = [](const at::Tensor& t) { return (double)t.stride(0) * t.size(0) * 4.0 < 4294967296.0; };
+  const bool dma = g_f32_dma && fits(a) && fits(b);
   const hipStream_t st = ft_stream();
   if (a_t) {
-    if (b_t) launch_lay<true, true>(p, res, pt, st); else launch_lay<true, false>(p, res, pt, st);
+    if (b_t) launch_lay<true, true>(p, res, pt, dma, st); else launch_lay<true, false>(p, res, pt, dma, st);
   } else {
-    if (b_t) launch_lay<false, true>(p, res, pt, st); else launch_lay<false, false>(p, res, pt, st);
+    if (b_t) launch_lay<false, true>(p, res, pt, dma, st); else launch_lay<false, false>(p, res, pt, dma, st);
   }
   FT_LAUNCH_CHECK();
   return c;
 }
 
 void gemm_f32_set_splitk(int64_t s) { g_f32_splitk = (int)s; }
+void gemm_f32_set_dma(int64_t on) { g_f32_dma = (int)on; }
 int64_t gemm_f32_slices(int64_t M, int64_t N, int64_t K) {
   return f32_slices((int)(((M + BM - 1) / BM) * ((N + BN - 1) / BN)), (int)(K / BK));
 }
 
 TORCH_LIBRARY_FRAGMENT(ftamd, m) {
   m.def("gemm_f32_set_splitk(int s) -> ()", &gemm_f32_set_splitk);
+  m.def("gemm_f32_set_dma(int on) -> ()", &gemm_f32_set_dma);
   m.def("gemm_f32_slices(int M, int N, int K) -> int", &gemm_f32_slices);
   m.def(
       "gemm_f32(Tensor a, bool a_t, Tensor b, bool b_t, int M, int N, int K, Tensor(a!)? out=None, "

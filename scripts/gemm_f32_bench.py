@@ -2,7 +2,7 @@
 operands, as the fp32 model path called it before) on the products of an fp32 GPT-2-small /
 -medium / Llama-3-8B layer at T = 2048 tokens. Event-timed, median of 20 after 5 warm-up calls.
 
-    python scripts/gemm_f32_bench.py
+    python scripts/gemm_f32_bench.py [--dma 0|1]
 """
 import os
 import sys
@@ -30,6 +30,8 @@ def timeit(f, reps=20, warm=5):
 
 def main():
     K_ = kernels()
+    if len(sys.argv) > 2 and sys.argv[1] == "--dma":  # A/B: LDS-DMA form (1, default) or registers (0)
+        K_.gemm_f32_set_dma(int(sys.argv[2]))
     T = 2048
     cfgs = {"gpt2-small": (768, 2048, 50304), "gpt2-medium": (1024, 2816, 50304), "llama3-8b": (4096, 14336, 131072)}
     print(f"{'product':28s} {'M':>6} {'N':>6} {'K':>6} | {'f32 mfma us':>11} {'TF/s':>6} | {'hipBLASLt us':>12} {'TF/s':>6} | ratio")

@@ -147,3 +147,20 @@ def test_split_plan_fills_the_chip():
     assert k.gemm_f32_slices(2048, 768, 3072) > 1
     assert k.gemm_f32_slices(2048, 768, 4096) * 96 <= 512
     assert k.gemm_f32_slices(2048, 768, 128) == 1  # too shallow to split
+
+
+@pytest.mark.parametrize("a_t,b_t", LAYOUTS)
+def test_register_form_matches_the_dma_form(a_t, b_t):
+    """The register round-trip form (gemm_f32_set_dma(0): operands larger than 32-bit buffer offsets)
+    and the LDS-DMA form give the same exact products, tails included."""
+    M, N, Kd = 516, 260, 192
+    a, b, ref = operands(M, N, Kd, a_t, b_t, True)
+    k = K()
+    try:
+        outs = []
+        for dma in (1, 0):
+            k.gemm_f32_set_dma(dma)
+            outs.append(k.gemm_f32(a, a_t, b, b_t, M, N, Kd))
+    finally:
+        k.gemm_f32_set_dma(1)
+    assert torch.equal(outs[0].double(), ref) and torch.equal(outs[1].double(), ref)
