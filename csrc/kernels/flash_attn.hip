@@ -1026,6 +1026,7 @@ struct GqaFold {
   const float* sin_t;
   int dbg;                 // timing experiments only: 1 no fold work, 2 no release fence
   int q_done;              // dQ already rotated by the dQ kernel
+  int krot;                // no GQA (direct stores into dqkv): dK rotated back in the dK/dV kernel's store
 };
 
 // The fold of `rows` rows from t0 (one key tile of kv head kvh) by NT threads: 16-B units (8
@@ -1353,7 +1354,14 @@ __global__ __launch_bounds__(64 * NW * SPLIT, SPLIT == 1 ? 4 / NW : 8 / (NW * SP
       for (int r = 0; r < 16; ++r) {
         const int kr = (r & 3) + 8 * (r >> 2) + 4 * hi;
         const int d = db * 32 + l32;
-        *reinterpret_cast<bf16_t*>(stg + at(kr, d)) = cvt1<E>(dk[db][r] * scale);
+        float x = dk[db][r] * scale;
+        if (fold.krot) {  // (uniform) RoPE backward of dK, the interleaved pair (d, d ^ 1) in lanes l, l ^ 1
+          const float y = __shfl_xor(x, 1, 64);
+          const long pos = min(kw + kr, S - 1);
+          const float c = fold.cos_t[pos * (D / 2) + (d >> 1)], sn = fold.sin_t[pos * (D / 2) + (d >> 1)];
+          x = (d & 1) ? fmaf(-y, sn, x * c) : fmaf(x, c, y * sn);  // as the dQ kernel's rotation
+        }
+        *reinterpret_cast<bf16_t*>(stg + at(kr, d)) = cvt1<E>(x);
         *reinterpret_cast<bf16_t*>(stg + 32 * D * 2 + at(kr, d)) = cvt1<E>(dv[db][r]);
       }
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's staging writes landed
@@ -1665,6 +1673,14 @@ bool g_dkdv2_64 = false;
 // as a 128-block tail behind the heaviest key tiles (profiles/r4_flash_gqa_fold_probe.log).
 bool g_bwd_fold = false;
 
+// No-GQA backward (GPT-2-sized presets): dQ rotated in the dQ kernel's store and dK in the dK/dV
+// kernel's, so no separate rope_bwd_ pass (3 kernels per layer); flash_set_direct_rope(false): the
+// pass after the two kernels (A/B).
+bool g_direct_rope = [] {
+  const char* e = std::getenv("FT_FLASH_DIRECT_ROPE");
+  return e == nullptr || std::atoi(e) != 0;
+}();
+
 // The fold's per-tile arrival counters: one zeroed int32 buffer per device, grown on demand and
 // kept (each tile's last block re-arms its counter, so the buffer is zero between launches). One
 // backward in flight per device at a time (the training step's single compute stream). Under
@@ -1814,11 +1830,14 @@ at::Tensor flash_bwd(const at::Tensor& dout, const at::Tensor& qk, const at::Ten
   }();
   // RoPE backward of dQ in the dQ kernel's epilogue (deterministic mode, GQA partials to fold; the
   // direct no-GQA path rotates Q and K in one rope_bwd_ pass)
-  const bool q_rot = rope && det && !direct;
+  // (no GQA: the dK rotation too happens in the dK/dV kernel's store, so no rope_bwd_ pass follows;
+  // flash_set_direct_rope(false) restores that pass, for A/B)
+  const bool krot = rope && direct && g_direct_rope;
+  const bool q_rot = rope && det && (!direct || krot);
   const float* dq_cos = q_rot ? cptr<float>(*cos_t) : nullptr;
   const float* dq_sin = q_rot ? cptr<float>(*sin_t) : nullptr;
   GqaFold fold{nullptr, mptr<bf16_t>(dqkv), rope ? cptr<float>(*cos_t) : nullptr,
-               rope ? cptr<float>(*sin_t) : nullptr, fold_dbg, q_rot ? 1 : 0};
+               rope ? cptr<float>(*sin_t) : nullptr, fold_dbg, q_rot ? 1 : 0, krot ? 1 : 0};
   // the in-kernel fold holds at most 8 q-head partials per unit (uint4 x[U][8]): wider groups
   // take the finalize pass
   if (use_dkdv2 && !direct && g_bwd_fold && Hq / Hkv <= 8)
@@ -1890,8 +1909,8 @@ at::Tensor flash_bwd(const at::Tensor& dout, const at::Tensor& qk, const at::Ten
 #undef FT_DQ
 #undef FT_PRE
   FT_LAUNCH_CHECK();
-  if (direct) {  // no GQA partials to fold: only the RoPE backward remains
-    if (rope) rope_bwd_(dqkv, *cos_t, *sin_t, S, Hq, Hkv, D);
+  if (direct) {  // no GQA partials to fold: only the RoPE backward remains (unless done in-kernel)
+    if (rope && !krot) rope_bwd_(dqkv, *cos_t, *sin_t, S, Hq, Hkv, D);
     return dqkv;
   }
   if (fold.cnt != nullptr) return dqkv;  // folded by the dK/dV kernel's last block per tile
@@ -1925,6 +1944,7 @@ void flash_set_fwd_prof(const std::optional<at::Tensor>& buf) {
 }
 void flash_set_kv_split(int64_t v) { g_kv_split = (int)v; }
 void flash_set_bwd_fold(bool on) { g_bwd_fold = on; }
+void flash_set_direct_rope(bool on) { g_direct_rope = on; }
 
 TORCH_LIBRARY_FRAGMENT(ftamd, m) {
   m.def("flash_set_dkdv2(bool on) -> ()", &flash_set_dkdv2);
@@ -1934,6 +1954,7 @@ TORCH_LIBRARY_FRAGMENT(ftamd, m) {
   m.def("flash_set_fwd_prof(Tensor? buf) -> ()", &flash_set_fwd_prof);
   m.def("flash_set_kv_split(int v) -> ()", &flash_set_kv_split);
   m.def("flash_set_bwd_fold(bool on) -> ()", &flash_set_bwd_fold);
+  m.def("flash_set_direct_rope(bool on) -> ()", &flash_set_direct_rope);
   m.def("flash_fwd(Tensor qk, Tensor qkv, int S, int Hq, int Hkv, int D) -> (Tensor, Tensor)",
         &flash_fwd);
   m.def(

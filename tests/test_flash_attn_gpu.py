@@ -224,11 +224,13 @@ def test_flash_dkdv_split_matches(B, S, Hq, Hkv, D):
 
 
 @pytest.mark.parametrize("B,S,Hq,Hkv,D,mode", [(1, 2048, 32, 8, 128, 1), (1, 512, 8, 2, 64, 1), (2, 256, 4, 4, 64, 1),
-                                              (1, 1000, 4, 2, 128, 0), (2, 512, 12, 12, 64, 1)])
+                                              (1, 1000, 4, 2, 128, 0), (2, 512, 12, 12, 64, 1),
+                                              (1, 1024, 8, 8, 128, 1), (1, 300, 16, 16, 64, 1)])
 def test_flash_bwd_with_rope_backward(B, S, Hq, Hkv, D, mode):
     """flash_bwd(..., cos, sin): the gradient of the UNROTATED projection, the RoPE backward done
-    in the pass that folds the GQA partials (or by rope_bwd_ when there is nothing to fold) ==
-    flash_bwd then rope_bwd_ (reference model.py:100-126) within one bf16 rounding; deterministic."""
+    in the pass that folds the GQA partials, or -- no GQA -- in the dQ and dK/dV kernels' stores
+    (round 6: no rope_bwd_ pass) == flash_bwd then rope_bwd_ (reference model.py:100-126) within one
+    bf16 rounding; deterministic."""
     from fault_tolerant_llm_training_amd._native import kernels
     from fault_tolerant_llm_training_amd.models.llama import rope_tables
 
@@ -312,3 +314,28 @@ def test_flash_fwd_timing_probe():
     finally:
         K.flash_set_fwd_prof(None)
         K.flash_set_fwd_split(-1)
+
+
+@pytest.mark.parametrize("S,H,D", [(512, 12, 64), (1024, 8, 128)])
+def test_no_gqa_rope_in_kernel_matches_the_separate_pass(S, H, D):
+    """No GQA: dQ / dK rotated back inside the two backward kernels (default) vs the separate
+    rope_bwd_ pass after them (flash_set_direct_rope(False)): one rounding instead of two, so equal
+    within bf16; dV identical."""
+    from fault_tolerant_llm_training_amd._native import kernels
+    from fault_tolerant_llm_training_amd.models.llama import rope_tables
+
+    K = kernels()
+    torch.manual_seed(5)
+    qkv = torch.randn(S, 3 * H * D, device="cuda").bfloat16()
+    qk = torch.randn(S, 2 * H * D, device="cuda").bfloat16()
+    do = torch.randn(S, H * D, device="cuda").bfloat16()
+    cos, sin = (t.cuda() for t in rope_tables(D, S, 10000.0))
+    o, lse = K.flash_fwd(qk, qkv, S, H, H, D)
+    got = K.flash_bwd(do, qk, qkv, o, lse, S, H, H, D, 1, cos, sin)
+    try:
+        K.flash_set_direct_rope(False)
+        sep = K.flash_bwd(do, qk, qkv, o, lse, S, H, H, D, 1, cos, sin)
+    finally:
+        K.flash_set_direct_rope(True)
+    assert rel(got[:, : 2 * H * D], sep[:, : 2 * H * D]) < 4e-3
+    assert torch.equal(got[:, 2 * H * D:], sep[:, 2 * H * D:])
