@@ -304,6 +304,10 @@ def build_model(args: TransformerModelArgs, device, dtype=torch.bfloat16, seed: 
     return Transformer(args).materialize(device, dtype, seed)
 
 
+# Dense matrix-core peaks of one MI355X per model dtype (no 2:1 sparsity): the MFU denominator
+PEAK_FLOPS = {torch.bfloat16: 2.5e15, torch.float16: 2.5e15, torch.float32: 157.3e12, torch.float64: 78.6e12}
+
+
 def flops_per_token(a: TransformerModelArgs, seq_len: int) -> float:
     """Training FLOPs/token: 6 × matmul params + causal attention (fwd+bwd = 3 × fwd)."""
     d, L, hd = a.dim, a.n_layers, a.head_dim

@@ -76,12 +76,14 @@ class _LossLog:
     consecutive log events (the host runs ahead of the GPU).
     """
 
-    def __init__(self, device: torch.device, tokens_per_step: int, world: int, flops_per_token: float):
+    def __init__(self, device: torch.device, tokens_per_step: int, world: int, flops_per_token: float,
+                 peak_flops: float = 2.5e15):
         self.cuda = device.type == "cuda"
         self.pending = []  # [step, host values, event or host time, extra]
         self.tokens = tokens_per_step
         self.world = world
         self.fpt = flops_per_token
+        self.peak = peak_flops  # the model dtype's dense matrix-core peak (models.llama.PEAK_FLOPS)
         self.last = None  # (step, event or host time)
 
     def push(self, step: int, loss: torch.Tensor, extra: Dict[str, Any], norm=None):
@@ -124,7 +126,7 @@ class _LossLog:
             extra["step_ms"] = f"{dt * 1e3:.1f}"
             extra["tok/s"] = f"{tok_s:.0f}"
             if self.cuda:
-                extra["MFU"] = f"{tok_s / self.world * self.fpt / 2.5e15:.3f}"
+                extra["MFU"] = f"{tok_s / self.world * self.fpt / self.peak:.3f}"
         self.last = (step, ev)
         if extra:
             msg += " | " + " | ".join(f"{k}: {v}" for k, v in extra.items())
@@ -471,7 +473,9 @@ def train(args) -> int:
     B, S, W = args.batch_size, args.sequence_length, info.world_size
     K = max(1, int(args.grad_accum))
     fpt = flops_per_token(margs, S)
-    losslog = _LossLog(device, B * K * S * W, W, fpt)
+    from .models.llama import PEAK_FLOPS
+
+    losslog = _LossLog(device, B * K * S * W, W, fpt, PEAK_FLOPS.get(model_dtype, 2.5e15))
     synthetic_counts = args.synthetic_data  # no ignore_index labels: the global count is static
     inv_static = None
     if synthetic_counts:
