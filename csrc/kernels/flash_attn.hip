@@ -1129,15 +1129,20 @@ __device__ __forceinline__ void gqa_fold_rows(const bf16_t* __restrict__ dk_part
 // SPLIT = 2: two half-blocks take alternate slice pairs of the same keys and add their dK / dV
 // partials through LDS at the end (fixed order: bit-reproducible), halving the longest
 // (first) key block's sweep.
-template <class E, int D, int NW = 4, int SPLIT = 1>
+// SD (self delta, the 3-kernel GQA backward): each slice's O rows come in by LDS-DMA beside its dO
+// rows and every wave forms the slice's delta = rowsum(dO * O) itself (the dQ kernel's arithmetic,
+// term for term: bitwise the same values), so this kernel runs FIRST and the dQ kernel after it
+// folds the GQA partials (no finalize pass).
+template <class E, int D, int NW = 4, int SPLIT = 1, bool SD = false>
 __global__ __launch_bounds__(64 * NW * SPLIT, SPLIT == 1 ? 4 / NW : 8 / (NW * SPLIT)) void flash_bwd_dkdv2_kernel(
     const bf16_t* __restrict__ dO, const bf16_t* __restrict__ qk, const bf16_t* __restrict__ qkv,
     const float* __restrict__ lse2, const float* __restrict__ delta, bf16_t* __restrict__ dk_part,
     bf16_t* __restrict__ dv_part, long ldkv, int B, int S, int Hq, int Hkv, float sl2, float scale, long ldqk_,
-    GqaFold fold) {
+    GqaFold fold, const bf16_t* __restrict__ O = nullptr) {
   constexpr int BK = 32 * NW, BQ = 32, KS = D / 16, NDB = D / 32;
   constexpr int QIMG = BQ * D * 2;          // one Q or dO slice
-  constexpr int SLOT = 2 * QIMG + 256;      // Q | dO | lse[32] | delta[32] of one slice
+  constexpr int STO = (SD ? 3 : 2) * QIMG;  // lse[32] | delta[32] after Q | dO (| O)
+  constexpr int SLOT = STO + 256;           // one slice
   __shared__ __attribute__((aligned(16))) char pb0[2 * SLOT * SPLIT];  // pair buffer 0: slice A | slice B
   __shared__ __attribute__((aligned(16))) char pb1[2 * SLOT * SPLIT];  // pair buffer 1 (per half-block)
 
@@ -1160,6 +1165,7 @@ __global__ __launch_bounds__(64 * NW * SPLIT, SPLIT == 1 ? 4 / NW : 8 / (NW * SP
   const bf16_t* dOg = dO + (long)b * S * ldo + (long)h * D;
   const float* lseg = lse2 + ((long)b * Hq + h) * stat_stride(S);
   const float* delg = delta + ((long)b * Hq + h) * stat_stride(S);
+  const bf16_t* Og = SD ? O + (long)b * S * ldo + (long)h * D : nullptr;
 
   typename FA<E>::v8 vf[KS], kf[KS];
   {
@@ -1190,11 +1196,12 @@ __global__ __launch_bounds__(64 * NW * SPLIT, SPLIT == 1 ? 4 / NW : 8 / (NW * SP
           const long q = min(q0 + r, S - 1);
           glds16(Qg + q * ldqk + c * 8, sl + piece * 1024);
           glds16(dOg + q * ldo + c * 8, sl + QIMG + piece * 1024);
+          if constexpr (SD) glds16(Og + q * ldo + c * 8, sl + 2 * QIMG + piece * 1024);
         });
-        if (wave == half && lane < 16) {
+        if (wave == half && lane < (SD ? 8 : 16)) {
           // lanes 0-7: lse rows q0..q0+31, lanes 8-15: delta (rows padded to 32: in bounds)
           const float* src = lane < 8 ? lseg + q0 + 4 * lane : delg + q0 + 4 * (lane - 8);
-          glds16(src, sl + 2 * QIMG);
+          glds16(src, sl + STO);
         }
       }
     }
@@ -1217,13 +1224,34 @@ __global__ __launch_bounds__(64 * NW * SPLIT, SPLIT == 1 ? 4 / NW : 8 / (NW * SP
       sv = mfma32(ld_row<E, D>(qi, l32, 2 * ks + hi), kf[ks], sv);
       dpv = mfma32(ld_row<E, D>(di, l32, 2 * ks + hi), vf[ks], dpv);
     }
+    if constexpr (SD) {
+      // delta of query row l32 of the slice, as flash_bwd_dq_kernel forms it: this lane's half of
+      // the dO . O dot product (columns 16 ks + 8 hi ..), plus lane ^ 32's; every wave writes the
+      // same 32 values into the slot's delta row, read back by its own fin (LDS is in order per wave)
+      const char* oi = sl + 2 * QIMG;
+      float acc = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const auto dv = ld_row<E, D>(di, l32, 2 * ks + hi);
+        const auto ov = ld_row<E, D>(oi, l32, 2 * ks + hi);
+        float x[8], y[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) x[j] = (float)dv[j];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) y[j] = (float)ov[j];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc += x[j] * y[j];
+      }
+      const float dl = acc + __shfl_xor(acc, 32, 64);
+      if (hi == 0) reinterpret_cast<float*>(const_cast<char*>(sl) + STO)[BQ + l32] = dl;
+    }
   };
   auto fin = [&](const char* sl, const int i, f32x16_t sv, f32x16_t dpv, auto MASKED)
       __attribute__((always_inline)) {
     constexpr bool MASK = decltype(MASKED)::value;
     const char* qi = sl;
     const char* di = sl + QIMG;
-    const float* st = reinterpret_cast<const float*>(sl + 2 * QIMG);
+    const float* st = reinterpret_cast<const float*>(sl + STO);
     const int qb = (qs0 + i) * BQ;
     static_for<4>([&](auto G) {
       constexpr int g = G;
@@ -1418,7 +1446,8 @@ __global__ __launch_bounds__(64 * NW * SPLIT, SPLIT == 1 ? 4 / NW : 8 / (NW * SP
     const bf16_t* __restrict__ dO, const bf16_t* __restrict__ qk, const bf16_t* __restrict__ qkv,
     const float* __restrict__ lse2, float* __restrict__ delta, bf16_t* __restrict__ dqkv, int B,
     int S, int Hq, int Hkv, float sl2, float scale, long ldqk_, const bf16_t* __restrict__ O,
-    const float* __restrict__ cos_t, const float* __restrict__ sin_t) {
+    const float* __restrict__ cos_t, const float* __restrict__ sin_t,
+    const bf16_t* __restrict__ dk_part = nullptr, const bf16_t* __restrict__ dv_part = nullptr) {
   constexpr int BM = 32 * NW, BN = 64, KS = D / 16, NDB = D / 32;
   constexpr int TILE = BN * D * 2;
   // K | V tiles arrive by LDS-DMA (no staging VGPRs held across the compute: at one wave
@@ -1609,6 +1638,55 @@ __global__ __launch_bounds__(64 * NW * SPLIT, SPLIT == 1 ? 4 / NW : 8 / (NW * SP
       return (i & 1) ? fmaf(-a0, sn, b0 * c) : fmaf(a0, c, b0 * sn);
     });
   }
+
+  if (dk_part != nullptr) {  // (uniform) the 3-kernel GQA backward: the dK/dV kernel ran first
+    // Fold of its per-q-head partials: this block takes key rows [qt BM, +BM) of kv head kvh and
+    // column slice gi (D / G columns) of dK and dV: the sum over the G q-heads in head order, dK
+    // rotated back (RoPE), as flash_bwd_finalize_kernel / gqa_fold_rows compute it (bitwise).
+    // (SPLIT = 2: half-block 1 has returned; the 64 NW threads of half 0 do it.)
+    const int G = Hq / Hkv, gi = h - kvh * G;
+    const int cps = D / G / 8;  // 16-B chunks per column slice
+    const int r0 = qt * BM, nr = min(BM, S - r0);
+    const long W = (long)(Hq + 2 * Hkv) * D;
+    const int n = nr * 2 * cps;
+    for (int i = tid; i < n; i += 64 * NW) {
+      const int row = i / (2 * cps), u = i - row * 2 * cps;
+      const bool isk = u < cps;
+      const int c = (gi * cps + (isk ? u : u - cps)) * 8;  // first column within the head
+      const long t = (long)b * S + r0 + row;
+      const bf16_t* src = (isk ? dk_part : dv_part) + t * Hq * D + (long)kvh * G * D + c;
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = 0.f;
+      for (int g = 0; g < G; ++g) {
+        const uint4 q = *reinterpret_cast<const uint4*>(src + g * D);
+        const unsigned w4[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[2 * e] = v[2 * e] + u16f<E>(w4[e]);
+          v[2 * e + 1] = v[2 * e + 1] + u16f<E>(w4[e] >> 16);
+        }
+      }
+      if (isk && cos_t != nullptr) {
+        const long pos = r0 + row;
+        const float4 c4 = *reinterpret_cast<const float4*>(cos_t + pos * (D / 2) + (c >> 1));
+        const float4 s4 = *reinterpret_cast<const float4*>(sin_t + pos * (D / 2) + (c >> 1));
+        const float cc[4] = {c4.x, c4.y, c4.z, c4.w}, ss[4] = {s4.x, s4.y, s4.z, s4.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float a = v[2 * e], bb = v[2 * e + 1];
+          v[2 * e] = fmaf(a, cc[e], bb * ss[e]);
+          v[2 * e + 1] = fmaf(-a, ss[e], bb * cc[e]);
+        }
+      }
+      uint4 o;
+      o.x = pk2<E>(v[0], v[1]);
+      o.y = pk2<E>(v[2], v[3]);
+      o.z = pk2<E>(v[4], v[5]);
+      o.w = pk2<E>(v[6], v[7]);
+      *reinterpret_cast<uint4*>(dqkv + t * W + (isk ? (long)Hq * D : (long)(Hq + Hkv) * D) + (long)kvh * D + c) = o;
+    }
+  }
 }
 
 // dqkv[:, q | k | v] = bf16(dQ), bf16(sum_G dK_part), bf16(sum_G dV_part).
@@ -1676,6 +1754,17 @@ bool g_bwd_fold = false;
 // No-GQA backward (GPT-2-sized presets): dQ rotated in the dQ kernel's store and dK in the dK/dV
 // kernel's, so no separate rope_bwd_ pass (3 kernels per layer); flash_set_direct_rope(false): the
 // pass after the two kernels (A/B).
+// GQA deterministic backward in 3 kernels (FT_FLASH_FOLD3=1 / flash_set_fold3(true)): the dK/dV
+// kernel first, forming delta itself from O (SD), then the dQ kernel, which also folds the GQA
+// partials (no finalize pass). Bitwise equal to the default 4-kernel order (dQ, dK/dV, finalize) but
+// slower at the 8B layer: 200.8 vs 165.7 us -- every wave of the dK/dV kernel forms its slices'
+// deltas on the critical path (88.6 -> 120.7 us), and the fold in the dQ kernel costs what the
+// finalize pass did (+11.6 vs 9.6 us) (profiles/r6/flash_fold3_ab.log). Off by default.
+bool g_fold3 = [] {
+  const char* e = std::getenv("FT_FLASH_FOLD3");
+  return e != nullptr && std::atoi(e) != 0;
+}();
+
 bool g_direct_rope = [] {
   const char* e = std::getenv("FT_FLASH_DIRECT_ROPE");
   return e == nullptr || std::atoi(e) != 0;
@@ -1842,6 +1931,11 @@ at::Tensor flash_bwd(const at::Tensor& dout, const at::Tensor& qk, const at::Ten
   // take the finalize pass
   if (use_dkdv2 && !direct && g_bwd_fold && Hq / Hkv <= 8)
     fold.cnt = fold_counters(qk.device(), (long)B * Hkv * ((S + 32 * nw_ - 1) / (32 * nw_)));
+  // 3-kernel GQA backward (g_fold3): dK/dV first (delta from O), then dQ + the fold; a column slice
+  // of D / G columns per q-head block must be whole 16-B chunks
+  const bool fold3 = use_dkdv2 && !direct && g_fold3 && fold.cnt == nullptr && D % (8 * (Hq / Hkv)) == 0;
+  const bf16_t* fkp = fold3 ? dkp : nullptr;
+  const bf16_t* fvp = fold3 ? dvp : nullptr;
   const int pre_blocks = (int)((rows * 16 + 255) / 256);
   const int nkt = (S + 127) / 128;
   dim3 grid(nkt * B * Hq), block(256);
@@ -1858,10 +1952,16 @@ at::Tensor flash_bwd(const at::Tensor& dout, const at::Tensor& qk, const at::Ten
   // forces; default: grids of at most one wave per SIMD
   const bool kv_split = D == 64 && (g_kv_split >= 0 ? g_kv_split == 1 : (long)grid2.x * nw <= 1024);
 #define FT_DKDV2(DD, NW_, SP_)                                                                             \
-  hipLaunchKernelGGL((flash_bwd_dkdv2_kernel<E, DD, NW_, SP_>), grid2, dim3(64 * NW_ * SP_), 0, ft_stream(), \
-                     cptr<bf16_t>(dout), cptr<bf16_t>(qk), cptr<bf16_t>(qkv), cptr<float>(lse),           \
-                     cptr<float>(delta), dkp, dvp, ldkv, B, (int)S,                                       \
-                     (int)Hq, (int)Hkv, sl2, scale, ldqk, fold)
+  if (fold3)                                                                                                 \
+    hipLaunchKernelGGL((flash_bwd_dkdv2_kernel<E, DD, NW_, SP_, true>), grid2, dim3(64 * NW_ * SP_), 0,        \
+                       ft_stream(), cptr<bf16_t>(dout), cptr<bf16_t>(qk), cptr<bf16_t>(qkv), cptr<float>(lse), \
+                       cptr<float>(delta), dkp, dvp, ldkv, B, (int)S, (int)Hq, (int)Hkv, sl2, scale, ldqk, fold, \
+                       cptr<bf16_t>(out));                                                                   \
+  else                                                                                                       \
+    hipLaunchKernelGGL((flash_bwd_dkdv2_kernel<E, DD, NW_, SP_>), grid2, dim3(64 * NW_ * SP_), 0, ft_stream(), \
+                       cptr<bf16_t>(dout), cptr<bf16_t>(qk), cptr<bf16_t>(qkv), cptr<float>(lse),         \
+                       cptr<float>(delta), dkp, dvp, ldkv, B, (int)S,                                     \
+                       (int)Hq, (int)Hkv, sl2, scale, ldqk, fold, nullptr)
   // dQ key split by default (FT_FLASH_DQ_SPLIT=0 turns it off): S = 2048, 12 heads of 64:
   // 94 -> 83 us for the whole backward; 8B layer 173 -> 167 us; S = 16384 1006 -> 972 us
   // (profiles/r2_flash_key_split.log)
@@ -1873,33 +1973,45 @@ at::Tensor flash_bwd(const at::Tensor& dout, const at::Tensor& qk, const at::Ten
     hipLaunchKernelGGL((flash_bwd_dq_kernel<E, DD, NW_, 2>), grid2, dim3(128 * NW_), 0, ft_stream(),       \
                        cptr<bf16_t>(dout), cptr<bf16_t>(qk), cptr<bf16_t>(qkv), cptr<float>(lse),       \
                        mptr<float>(delta), mptr<bf16_t>(dqkv), B, (int)S, (int)Hq, (int)Hkv, sl2, scale, ldqk, \
-                       cptr<bf16_t>(out), dq_cos, dq_sin);                                              \
+                       cptr<bf16_t>(out), dq_cos, dq_sin, fkp, fvp);                                    \
   else                                                                                                  \
     hipLaunchKernelGGL((flash_bwd_dq_kernel<E, DD, NW_, 1>), grid2, block2, 0, ft_stream(),                \
                        cptr<bf16_t>(dout), cptr<bf16_t>(qk), cptr<bf16_t>(qkv), cptr<float>(lse),       \
                        mptr<float>(delta), mptr<bf16_t>(dqkv), B, (int)S, (int)Hq, (int)Hkv, sl2, scale, ldqk, \
-                       cptr<bf16_t>(out), dq_cos, dq_sin)
+                       cptr<bf16_t>(out), dq_cos, dq_sin, fkp, fvp)
+  // the two deterministic kernels in their order: dQ first (it forms delta for the dK/dV kernel), or
+  // -- fold3 -- dK/dV first (forms delta itself) and dQ after it (folds the partials it wrote)
+#define FT_PAIR(DQ_STMT, KV_STMT) \
+  if (fold3) {                    \
+    KV_STMT;                      \
+    DQ_STMT;                      \
+  } else {                        \
+    DQ_STMT;                      \
+    KV_STMT;                      \
+  }
 #define FT_PRE(DD)                                                                                      \
   hipLaunchKernelGGL((flash_bwd_pre_kernel<E, DD>), dim3(pre_blocks), block, 0, ft_stream(),             \
                      cptr<bf16_t>(dout), cptr<bf16_t>(out), mptr<float>(delta), B, (int)S, (int)Hq)
   FT_DISPATCH_E16(qk.scalar_type(), {
     if (D == 128) {
       if (mode == 0) { FT_PRE(128); FT_BWD(128, 0); }
-      else if (mode == 1) { FT_DQ(128, 4); if (g_dkdv2 && nw == 4) { FT_DKDV2(128, 4, 1); } else FT_BWD(128, 1); }
+      else if (mode == 1) {
+        if (g_dkdv2 && nw == 4) { FT_PAIR({ FT_DQ(128, 4); }, { FT_DKDV2(128, 4, 1); }) }
+        else { FT_DQ(128, 4); FT_BWD(128, 1); }
+      }
       else { FT_PRE(128); FT_BWD(128, 2); }
     } else {
       if (mode == 0) { FT_PRE(64); FT_BWD(64, 0); }
       else if (mode == 1 && nw == 2) {
-        FT_DQ(64, 2);
-        if (kv_split) FT_DKDV2(64, 2, 2); else FT_DKDV2(64, 2, 1);
+        if (kv_split) { FT_PAIR({ FT_DQ(64, 2); }, { FT_DKDV2(64, 2, 2); }) }
+        else { FT_PAIR({ FT_DQ(64, 2); }, { FT_DKDV2(64, 2, 1); }) }
       }
       // head_dim 64 with 4-wave blocks: the one-slice dK/dV kernel is faster (S = 8192, 16 heads:
       // 631 vs 783 us, profiles/r2_flash_long_context.log); FT_FLASH_DKDV2=2 forces the slice pair
       else if (mode == 1) {
-        FT_DQ(64, 4);
-        if (g_dkdv2_64 && kv_split) FT_DKDV2(64, 4, 2);
-        else if (g_dkdv2_64) FT_DKDV2(64, 4, 1);
-        else FT_BWD(64, 1);
+        if (g_dkdv2_64 && kv_split) { FT_PAIR({ FT_DQ(64, 4); }, { FT_DKDV2(64, 4, 2); }) }
+        else if (g_dkdv2_64) { FT_PAIR({ FT_DQ(64, 4); }, { FT_DKDV2(64, 4, 1); }) }
+        else { FT_DQ(64, 4); FT_BWD(64, 1); }
       }
       else { FT_PRE(64); FT_BWD(64, 2); }
     }
@@ -1907,6 +2019,7 @@ at::Tensor flash_bwd(const at::Tensor& dout, const at::Tensor& qk, const at::Ten
 #undef FT_BWD
 #undef FT_DKDV2
 #undef FT_DQ
+#undef FT_PAIR
 #undef FT_PRE
   FT_LAUNCH_CHECK();
   if (direct) {  // no GQA partials to fold: only the RoPE backward remains (unless done in-kernel)
@@ -1914,6 +2027,7 @@ at::Tensor flash_bwd(const at::Tensor& dout, const at::Tensor& qk, const at::Ten
     return dqkv;
   }
   if (fold.cnt != nullptr) return dqkv;  // folded by the dK/dV kernel's last block per tile
+  if (fold3) return dqkv;                // folded by the dQ kernel
   const long vec = (long)T * ((Hq + 2 * Hkv) * D / 4);
   const int fin_blocks = (int)std::max(1L, std::min((vec + 255) / 256, 4096L));
   FT_DISPATCH_E16(qk.scalar_type(),
@@ -1945,6 +2059,7 @@ void flash_set_fwd_prof(const std::optional<at::Tensor>& buf) {
 void flash_set_kv_split(int64_t v) { g_kv_split = (int)v; }
 void flash_set_bwd_fold(bool on) { g_bwd_fold = on; }
 void flash_set_direct_rope(bool on) { g_direct_rope = on; }
+void flash_set_fold3(bool on) { g_fold3 = on; }
 
 TORCH_LIBRARY_FRAGMENT(ftamd, m) {
   m.def("flash_set_dkdv2(bool on) -> ()", &flash_set_dkdv2);
@@ -1955,6 +2070,7 @@ TORCH_LIBRARY_FRAGMENT(ftamd, m) {
   m.def("flash_set_kv_split(int v) -> ()", &flash_set_kv_split);
   m.def("flash_set_bwd_fold(bool on) -> ()", &flash_set_bwd_fold);
   m.def("flash_set_direct_rope(bool on) -> ()", &flash_set_direct_rope);
+  m.def("flash_set_fold3(bool on) -> ()", &flash_set_fold3);
   m.def("flash_fwd(Tensor qk, Tensor qkv, int S, int Hq, int Hkv, int D) -> (Tensor, Tensor)",
         &flash_fwd);
   m.def(

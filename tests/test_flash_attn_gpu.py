@@ -339,3 +339,30 @@ def test_no_gqa_rope_in_kernel_matches_the_separate_pass(S, H, D):
         K.flash_set_direct_rope(True)
     assert rel(got[:, : 2 * H * D], sep[:, : 2 * H * D]) < 4e-3
     assert torch.equal(got[:, 2 * H * D:], sep[:, 2 * H * D:])
+
+
+@pytest.mark.parametrize("B,S,Hq,Hkv,D,rope", [(1, 2048, 32, 8, 128, True), (2, 320, 8, 2, 128, False),
+                                               (1, 1000, 4, 1, 128, True), (2, 512, 8, 2, 64, True),
+                                               (1, 100, 6, 2, 64, False), (1, 777, 16, 2, 128, True)])
+def test_gqa_backward_in_three_kernels_equals_four(B, S, Hq, Hkv, D, rope):
+    """GQA deterministic backward in 3 kernels (flash_set_fold3(True): dK/dV first forming delta from
+    O, then dQ folding the per-q-head partials) == the default 4-kernel order (dQ, dK/dV, finalize),
+    bit for bit: delta, the fold order and the RoPE arithmetic are term-for-term the same."""
+    from fault_tolerant_llm_training_amd._native import kernels
+    from fault_tolerant_llm_training_amd.models.llama import rope_tables
+
+    K = kernels()
+    torch.manual_seed(S + Hq)
+    T = B * S
+    qkv = torch.randn(T, (Hq + 2 * Hkv) * D, device="cuda").bfloat16()
+    qk = torch.randn(T, (Hq + Hkv) * D, device="cuda").bfloat16()
+    do = torch.randn(T, Hq * D, device="cuda").bfloat16()
+    cs = tuple(t.cuda() for t in rope_tables(D, S, 500000.0)) if rope else (None, None)
+    o, lse = K.flash_fwd(qk, qkv, S, Hq, Hkv, D)
+    four = K.flash_bwd(do, qk, qkv, o, lse, S, Hq, Hkv, D, 1, *cs)
+    try:
+        K.flash_set_fold3(True)
+        three = K.flash_bwd(do, qk, qkv, o, lse, S, Hq, Hkv, D, 1, *cs)
+    finally:
+        K.flash_set_fold3(False)
+    assert torch.equal(three, four), (three.float() - four.float()).abs().max().item()
