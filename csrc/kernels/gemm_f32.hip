@@ -396,16 +396,20 @@ constexpr int RT = 1024;
 template <bool RES, bool PART>
 __global__ __launch_bounds__(RT) void f32_splitk_reduce(F32Args p) {
   __shared__ float red[RT / 64];
+  // without the tile's sum-of-squares partial a tile is 4 workgroups of 32 rows (the grids that split
+  // have few tiles: 4x the memory parallelism); with it, one workgroup sums the whole tile
+  constexpr int RS = PART ? 1 : 4, RB = BM / RS;
   const int tid = threadIdx.x;
-  const int tm = blockIdx.x % p.tiles_m, tn = blockIdx.x / p.tiles_m;
+  const int tile = blockIdx.x / RS, rb = (blockIdx.x % RS) * RB;
+  const int tm = tile % p.tiles_m, tn = tile / p.tiles_m;
   const long mn = (long)p.M * p.N;
   const bool vec = (p.N % 4 == 0) && (p.ldc % 4 == 0) && (!RES || p.ldr % 4 == 0);  // uniform
   float sq = 0.f;
   if (vec) {
 #pragma unroll
-    for (int q = 0; q < BM * BN / 4 / RT; ++q) {
+    for (int q = 0; q < RB * BN / 4 / RT; ++q) {
       const int e = q * RT + tid;
-      const int m = tm * BM + e / (BN / 4), n = tn * BN + 4 * (e % (BN / 4));
+      const int m = tm * BM + rb + e / (BN / 4), n = tn * BN + 4 * (e % (BN / 4));
       if (m >= p.M || n >= p.N) continue;
       const float* w = p.ws + (long)m * p.N + n;
       float4 x = *reinterpret_cast<const float4*>(w);
@@ -426,8 +430,8 @@ __global__ __launch_bounds__(RT) void f32_splitk_reduce(F32Args p) {
       *cp = x;
     }
   } else {
-    for (int e = tid; e < BM * BN; e += RT) {
-      const int m = tm * BM + e / BN, n = tn * BN + e % BN;
+    for (int e = tid; e < RB * BN; e += RT) {
+      const int m = tm * BM + rb + e / BN, n = tn * BN + e % BN;
       if (m >= p.M || n >= p.N) continue;
       const float* w = p.ws + (long)m * p.N + n;
       float x = w[0];
@@ -488,7 +492,7 @@ void launch_lay(const F32Args& p, bool res, bool part, bool dma, hipStream_t st)
   }
   if (p.ks > 1) {  // slices write raw partials: one instantiation, then the reduction's epilogue
     if (!dma) hipLaunchKernelGGL((gemm_f32_kernel<AT, BT, false, false>), g, b, 0, st, p);
-    const dim3 gr(p.tiles_m * p.tiles_n), br(RT);
+    const dim3 gr(p.tiles_m * p.tiles_n * (part ? 1 : 4)), br(RT);  // (RS of f32_splitk_reduce)
     if (res && part)
       hipLaunchKernelGGL((f32_splitk_reduce<true, true>), gr, br, 0, st, p);
     else if (res)
