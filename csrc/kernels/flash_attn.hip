@@ -1026,7 +1026,7 @@ struct GqaFold {
   const float* sin_t;
   int dbg;                 // timing experiments only: 1 no fold work, 2 no release fence
   int q_done;              // dQ already rotated by the dQ kernel
-  int krot;                // no GQA (direct stores into dqkv): dK rotated back in the dK/dV kernel's store
+  int krot;                // no GQA (direct stores into dqkv): dK rotated back in the dK/dV kernel's row stores
 };
 
 // The fold of `rows` rows from t0 (one key tile of kv head kvh) by NT threads: 16-B units (8
@@ -1382,14 +1382,7 @@ __global__ __launch_bounds__(64 * NW * SPLIT, SPLIT == 1 ? 4 / NW : 8 / (NW * SP
       for (int r = 0; r < 16; ++r) {
         const int kr = (r & 3) + 8 * (r >> 2) + 4 * hi;
         const int d = db * 32 + l32;
-        float x = dk[db][r] * scale;
-        if (fold.krot) {  // (uniform) RoPE backward of dK, the interleaved pair (d, d ^ 1) in lanes l, l ^ 1
-          const float y = __shfl_xor(x, 1, 64);
-          const long pos = min(kw + kr, S - 1);
-          const float c = fold.cos_t[pos * (D / 2) + (d >> 1)], sn = fold.sin_t[pos * (D / 2) + (d >> 1)];
-          x = (d & 1) ? fmaf(-y, sn, x * c) : fmaf(x, c, y * sn);  // as the dQ kernel's rotation
-        }
-        *reinterpret_cast<bf16_t*>(stg + at(kr, d)) = cvt1<E>(x);
+        *reinterpret_cast<bf16_t*>(stg + at(kr, d)) = cvt1<E>(dk[db][r] * scale);
         *reinterpret_cast<bf16_t*>(stg + 32 * D * 2 + at(kr, d)) = cvt1<E>(dv[db][r]);
       }
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's staging writes landed
@@ -1401,7 +1394,22 @@ __global__ __launch_bounds__(64 * NW * SPLIT, SPLIT == 1 ? 4 / NW : 8 / (NW * SP
       if (k < S) {
         const int so = r * (D * 2) + ((c ^ (r % CH)) << 4);
         const long off = ((long)b * S + k) * ldkv + (long)h * D + c * 8;
-        *reinterpret_cast<uint4*>(dk_part + off) = *reinterpret_cast<const uint4*>(stg + so);
+        uint4 kv = *reinterpret_cast<const uint4*>(stg + so);
+        if (fold.krot) {  // (uniform) RoPE backward of the 4 pairs of this dK chunk, as rope_bwd_ does it
+          const float4 c4 = *reinterpret_cast<const float4*>(fold.cos_t + (long)k * (D / 2) + c * 4);
+          const float4 s4 = *reinterpret_cast<const float4*>(fold.sin_t + (long)k * (D / 2) + c * 4);
+          const float cc[4] = {c4.x, c4.y, c4.z, c4.w}, ss[4] = {-s4.x, -s4.y, -s4.z, -s4.w};
+          float x[8], y[8];
+          unpack8e<E>(kv, x);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float a = x[2 * q], bb = x[2 * q + 1];
+            y[2 * q] = a * cc[q] - bb * ss[q];
+            y[2 * q + 1] = a * ss[q] + bb * cc[q];
+          }
+          kv = pack8e<E>(y);
+        }
+        *reinterpret_cast<uint4*>(dk_part + off) = kv;
         *reinterpret_cast<uint4*>(dv_part + off) = *reinterpret_cast<const uint4*>(stg + 32 * D * 2 + so);
       }
     }

@@ -319,8 +319,8 @@ def test_flash_fwd_timing_probe():
 @pytest.mark.parametrize("S,H,D", [(512, 12, 64), (1024, 8, 128)])
 def test_no_gqa_rope_in_kernel_matches_the_separate_pass(S, H, D):
     """No GQA: dQ / dK rotated back inside the two backward kernels (default) vs the separate
-    rope_bwd_ pass after them (flash_set_direct_rope(False)): one rounding instead of two, so equal
-    within bf16; dV identical."""
+    rope_bwd_ pass after them (flash_set_direct_rope(False)): dQ rotated in fp32 before its one
+    rounding (equal within bf16), dK rotated per 16-B chunk as rope_bwd_ does (bitwise), dV identical."""
     from fault_tolerant_llm_training_amd._native import kernels
     from fault_tolerant_llm_training_amd.models.llama import rope_tables
 
@@ -337,8 +337,8 @@ def test_no_gqa_rope_in_kernel_matches_the_separate_pass(S, H, D):
         sep = K.flash_bwd(do, qk, qkv, o, lse, S, H, H, D, 1, cos, sin)
     finally:
         K.flash_set_direct_rope(True)
-    assert rel(got[:, : 2 * H * D], sep[:, : 2 * H * D]) < 4e-3
-    assert torch.equal(got[:, 2 * H * D:], sep[:, 2 * H * D:])
+    assert rel(got[:, : H * D], sep[:, : H * D]) < 4e-3
+    assert torch.equal(got[:, H * D:], sep[:, H * D:])
 
 
 @pytest.mark.parametrize("B,S,Hq,Hkv,D,rope", [(1, 2048, 32, 8, 128, True), (2, 320, 8, 2, 128, False),
