@@ -1641,8 +1641,12 @@ __global__ __launch_bounds__(64 * NW * SPLIT, SPLIT == 1 ? 4 / NW : 8 / (NW * SP
     store_row16<E, NDB>(dqkv + ((long)b * S + pos) * ldv + (long)h * D, hi, qrow < S, [&](int db, int i) {
       const int i0 = i & ~1;
       const float a0 = dq[db][i0] * scale, b0 = dq[db][i0 + 1] * scale;
-      const int fi = (db * 32 + 8 * (i >> 2) + 4 * hi + (i & 3)) >> 1;
-      const float c = cos_t[pos * (D / 2) + fi], sn = sin_t[pos * (D / 2) + fi];
+      // the lane's 4 columns are 2 whole pairs: one float2 of cos / sin each (the 4 calls of a
+      // group load the same addresses, merged by the compiler) instead of 2 scalar loads per element
+      const int fb = (db * 32 + 8 * (i >> 2) + 4 * hi) >> 1;
+      const float2 c2 = *reinterpret_cast<const float2*>(cos_t + pos * (D / 2) + fb);
+      const float2 s2 = *reinterpret_cast<const float2*>(sin_t + pos * (D / 2) + fb);
+      const float c = (i & 2) ? c2.y : c2.x, sn = (i & 2) ? s2.y : s2.x;
       return (i & 1) ? fmaf(-a0, sn, b0 * c) : fmaf(a0, c, b0 * sn);
     });
   }
