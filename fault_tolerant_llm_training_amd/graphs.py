@@ -81,7 +81,12 @@ class GraphedStep:
             self.cap_stream = torch.cuda.Stream()
             with torch.cuda.stream(self.cap_stream):
                 kernels().gemm_w4_prepare_capture()
-        with torch.cuda.graph(g, stream=self.cap_stream):
+        # thread-local capture: in the default global mode any HIP call another thread makes while
+        # the capture is open fails -- the RCCL watchdog thread polling the events of earlier
+        # (already finished) collectives then got hipErrorCapturedEvent and took the process down
+        # (1 run in ~7 of the DP graph test, even with TORCH_NCCL_RETHROW_CUDA_ERRORS=0); only the
+        # capturing thread's own calls need the check
+        with torch.cuda.graph(g, stream=self.cap_stream, capture_error_mode="thread_local"):
             self._opt_step()  # (its host-side step count is reset below; hyper is read on device)
             self.loss = self.fwd_bwd(self.tok, self.lab)
             self._join()

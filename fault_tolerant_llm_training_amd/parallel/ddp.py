@@ -89,16 +89,16 @@ def set_fused_sumsq(on: bool) -> None:
     FUSED_SUMSQ = bool(on)
 
 
-def sink_partials(numel: int, ndim: int, shape=None) -> int:
+def sink_partials(numel: int, ndim: int, shape=None, tile_rows: int = 256) -> int:
     """Partial slots a sink's producers may write: one per output tile of a 2-D weight (w4: 256 x
-    >= 128, a tail tile of the dW layout covering fewer; the fp32 MFMA GEMM: 128 x 128 -- so
-    ceil(rows / 128) x ceil(cols / 128) bounds both), one per 32 columns of a 1-D one; also the grid
-    of the fallback sumsq pass."""
+    >= 128, a tail tile of the dW layout covering fewer: ceil(rows / 256) x ceil(cols / 128); the
+    fp32 MFMA GEMM's 128 x 128 tiles: tile_rows = 128), one per 32 columns of a 1-D one; also the grid
+    of the fallback sumsq pass. (Every slot enters norm_finish's sum: no more than the producers use.)"""
     if ndim <= 1:
         return max(1, (numel + 31) // 32)
     n = max(1, (numel + 32767) // 32768)
     if shape is not None and len(shape) == 2:
-        n = max(n, -(-int(shape[0]) // 128) * -(-int(shape[1]) // 128))
+        n = max(n, -(-int(shape[0]) // tile_rows) * -(-int(shape[1]) // 128))
     return n
 
 
@@ -231,7 +231,8 @@ class GradReducer:
             plain = [s for s in flat.sinks.values()
                      if not any(lo <= s.start and s.end <= hi for lo, hi in covered)]
             for sink in sorted(fused + plain, key=lambda s: s.start, reverse=True):
-                k = sink_partials(sink.end - sink.start, sink.buf.dim(), tuple(sink.buf.shape))
+                k = sink_partials(sink.end - sink.start, sink.buf.dim(), tuple(sink.buf.shape),
+                                  128 if sink.buf.dtype == torch.float32 else 256)
                 sink.part = (p, p + k)  # replaced by the tensor slice below
                 p += k
                 self._sq_sinks.append(sink)
