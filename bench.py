@@ -198,7 +198,10 @@ def main():
     if a.graph:
         if K > 1 or dev.type != "cuda":
             raise SystemExit("--graph: GPU ranks, no gradient accumulation")
-        from fault_tolerant_llm_training_amd.graphs import GraphedStep
+        from fault_tolerant_llm_training_amd.graphs import GraphedStep, hw_queue_problem
+
+        if hw_queue_problem():
+            raise SystemExit("--graph: " + hw_queue_problem())
 
         def fwd_bwd(tok, lab):
             loss_ = model(tok, lab, inv_count)

@@ -24,8 +24,21 @@ from typing import Callable, Optional
 
 import torch
 
+import os
+
 from ._native import kernels
 from .ops.functional import join_dw_stream
+
+
+def hw_queue_problem() -> str:
+    """Why the whole-step graph must not run under this process's HIP queue setting, or "". With
+    GPU_MAX_HW_QUEUES=2 the HIP runtime segfaults inside hipGraphLaunch on the replay of this
+    multi-stream graph (GPT-2-small, profiles/r6/hw_queues_ab.log); 8 queues replay 2.7x slower."""
+    q = os.environ.get("GPU_MAX_HW_QUEUES")
+    if q is not None and q.strip().isdigit() and int(q) < 4:
+        return (f"GPU_MAX_HW_QUEUES={q}: the HIP runtime crashes replaying the multi-stream step graph "
+                "with fewer than 4 hardware queues (leave it at the default 4)")
+    return ""
 
 
 class GraphedStep:

@@ -288,7 +288,9 @@ def train(args) -> int:
         # all-reduce -- the bucket collectives and ZeRO-1's parameter all-gathers are captured into
         # the graph; the per-step vote stays on the host, between replays). Host-side accumulation
         # or the fp64 path cannot be captured: there the flag is accepted and logged as not applied.
-        graphable = model_dtype in (torch.bfloat16, torch.float16, torch.float32)
+        from .graphs import hw_queue_problem
+
+        graphable = model_dtype in (torch.bfloat16, torch.float16, torch.float32) and not hw_queue_problem()
         if device.type == "cuda" and max(1, int(args.grad_accum)) == 1 and graphable:
             logger.info("Using `torch.compile`")
             logger.info("`torch.compile` -> whole-step HIP graph capture (--hip-graph): the step's "
@@ -298,7 +300,8 @@ def train(args) -> int:
             logger.info("Using `torch.compile` — accepted for CLI compatibility, not applied: the step "
                         "already runs fused gfx950 kernels and the whole-step HIP graph needs GPU ranks "
                         "without gradient accumulation, in a dtype the HIP kernels run (bf16/fp16/fp32: "
-                        "the fp64 composed path synchronises with the host inside the step)")
+                        "the fp64 composed path synchronises with the host inside the step)"
+                        + ("; " + hw_queue_problem() if hw_queue_problem() else ""))
     model.train()
 
     # AdamW moments default to the model dtype like the reference, except under fp16: the second
@@ -556,7 +559,10 @@ def train(args) -> int:
     if args.hip_graph:
         if K > 1 or device.type != "cuda" or model_dtype not in (torch.bfloat16, torch.float16, torch.float32):
             raise ValueError("--hip-graph: --grad-accum 1, --device cuda, --model-dtype bf16/fp16/fp32")
-        from .graphs import GraphedStep
+        from .graphs import GraphedStep, hw_queue_problem
+
+        if hw_queue_problem():
+            raise ValueError("--hip-graph: " + hw_queue_problem())
 
         inv_dev = torch.empty(1, dtype=torch.float32, device=device)  # static input of the graph
 
